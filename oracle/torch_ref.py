@@ -1,0 +1,111 @@
+"""Torch-CPU restatement of the reference synthesis path (the "port" CPU baseline).
+
+TEST INFRASTRUCTURE ONLY.  Used by ``tests/`` as a large-size checker and by
+``bench.py``'s ``cpu_baseline`` leg to time the reference's algorithm on the GPU
+box's host cores (the reference itself never travels to the box).  The product
+path never imports it.
+
+It issues the same ATen operator sequence as the reference on CPU tensors, so on
+the golden vectors it is bit-exact with the reference (``tests/test_oracle.py``).
+Each function cites the reference line it restates.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def scale_function(x):
+    # ddsp/core.py:77-78
+    return 2 * torch.sigmoid(x) ** (math.log(10)) + 1e-7
+
+
+def remove_above_nyquist(amplitudes, f0, sample_rate):
+    # ddsp/core.py:70-74
+    k = torch.arange(1, amplitudes.shape[-1] + 1).to(f0)
+    mask = (f0 * k < sample_rate / 2).float() + 1e-4
+    return amplitudes * mask
+
+
+def upsample(signal, factor):
+    # ddsp/core.py:64-67: nearest interpolation along time
+    y = F.interpolate(signal.permute(0, 2, 1), size=signal.shape[1] * factor)
+    return y.permute(0, 2, 1)
+
+
+def harmonic_synth(f0, amplitudes, sample_rate):
+    # ddsp/core.py:136-141
+    omega = torch.cumsum(2 * math.pi * f0 / sample_rate, 1)
+    k = torch.arange(1, amplitudes.shape[-1] + 1).to(omega)
+    return (torch.sin(omega * k) * amplitudes).sum(-1, keepdim=True)
+
+
+def amp_to_impulse_response(amp, target_size):
+    # ddsp/core.py:144-166
+    spec = torch.view_as_complex(torch.stack([amp, torch.zeros_like(amp)], -1))
+    h = torch.fft.irfft(spec)
+    n = h.shape[-1]
+    h = torch.roll(h, n // 2, -1) * torch.hann_window(n, dtype=h.dtype)
+    h = F.pad(h, (0, int(target_size) - int(n)))
+    return torch.roll(h, -n // 2, -1)
+
+
+def fft_convolve(signal, kernel):
+    # ddsp/core.py:169-176
+    s = F.pad(signal, (0, signal.shape[-1]))
+    k = F.pad(kernel, (kernel.shape[-1], 0))
+    y = torch.fft.irfft(torch.fft.rfft(s) * torch.fft.rfft(k))
+    return y[..., y.shape[-1] // 2:]
+
+
+class Reverb:
+    """ddsp/models/modules.py:7-35 (parameters passed in explicitly)."""
+
+    def __init__(self, noise, decay, wet, length, sample_rate):
+        self.noise, self.decay, self.wet = noise, decay, wet
+        self.length = length
+        self.t = (torch.arange(length) / sample_rate).reshape(1, -1, 1)
+
+    def build_impulse(self):
+        env = torch.exp(-F.softplus(-self.decay) * self.t * 500)
+        imp = self.noise * env * torch.sigmoid(self.wet)
+        imp[:, 0] = 1
+        return imp
+
+    def __call__(self, x):
+        imp = F.pad(self.build_impulse(), (0, 0, 0, x.shape[1] - self.length))
+        return fft_convolve(x.squeeze(-1), imp.squeeze(-1)).unsqueeze(-1)
+
+
+def harmonic_controls(amplitudes, dist, f0, sample_rate):
+    # ddsp/models/modules.py:44-67
+    amplitudes = scale_function(amplitudes)
+    dist = remove_above_nyquist(scale_function(dist), f0, sample_rate)
+    dist /= dist.sum(-1, keepdim=True)
+    return amplitudes, dist
+
+
+def harmonic_forward(amplitudes, dist, f0, block_size, sample_rate):
+    # ddsp/models/modules.py:69-80
+    dist *= amplitudes
+    return harmonic_synth(upsample(f0, block_size), upsample(dist, block_size), sample_rate)
+
+
+def noise_forward(magnitudes, noise, block_size):
+    # ddsp/models/modules.py:111-128 (controls already scaled; noise injected)
+    ir = amp_to_impulse_response(magnitudes, block_size)
+    y = fft_convolve(noise, ir).contiguous()
+    return y.reshape(y.shape[0], -1, 1)
+
+
+@torch.no_grad()
+def synth_path(f0, param, mags, noise, reverb, block_size, sample_rate):
+    """Frame-rate controls -> audio: the synthesis section of ddsp/models/decoder.py:106-125."""
+    amp, dist = harmonic_controls(param[..., :1], param[..., 1:], f0, sample_rate)
+    harmonic = harmonic_forward(amp, dist, f0, block_size, sample_rate)
+    mags = scale_function(mags + (-5.0))
+    noise_audio = noise_forward(mags, noise, block_size)
+    signal = harmonic + noise_audio
+    if reverb is not None:
+        signal = reverb(signal)
+    return signal

@@ -1,0 +1,196 @@
+"""Generate the golden parity fixtures by running the REFERENCE implementation.
+
+Test infrastructure only.  Run once, in the development container (the reference
+is not present on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+It imports hugofloresgarcia/ddsp_pytorch from /root/reference (read-only).  The
+reference's ``ddsp/core.py:5-6`` imports ``librosa`` and ``crepe`` and
+``ddsp/data.py:5`` imports ``pytorch_lightning``; none is installed and none is
+used on the synthesis path, so empty placeholder modules are put in
+``sys.modules`` for them (SURVEY.md §8(c) recipe).  Every number written below is
+computed by the reference's own functions and modules:
+
+* ``ddsp/core.py:64-176``   scale_function, remove_above_nyquist, upsample,
+                             harmonic_synth, amp_to_impulse_response, fft_convolve
+* ``ddsp/models/modules.py:7-128``  Reverb, HarmonicSynth, FilteredNoise
+* ``ddsp/models/decoder.py:76-136`` DDSPDecoder.forward
+
+Inputs follow SURVEY.md §8(d): f0 = 50*20**U[0,1) Hz, raw controls N(0,1),
+noise U[-1,1) drawn by ``torch.rand`` after ``torch.manual_seed(123)``, reverb
+parameters drawn after ``torch.manual_seed(1)``.  Only data (inputs and expected
+outputs) is written; nothing from the reference's source is stored.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def import_reference():
+    for name in ("librosa", "crepe"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    pl = types.ModuleType("pytorch_lightning")
+    pl.LightningDataModule = type("LightningDataModule", (), {})
+    sys.modules.setdefault("pytorch_lightning", pl)
+    sys.path.insert(0, REF)
+    import ddsp  # noqa: E402
+    from ddsp.models import modules, decoder  # noqa: E402
+    return ddsp, modules, decoder
+
+
+def synth_inputs(seed, B, F, H, NB):
+    g = torch.Generator().manual_seed(seed)
+    f0 = 50.0 * 20.0 ** torch.rand(B, F, 1, generator=g)
+    loudness = torch.randn(B, F, 1, generator=g)
+    param = torch.randn(B, F, H + 1, generator=g)
+    mags = torch.randn(B, F, NB, generator=g)
+    return f0, loudness, param, mags
+
+
+def save(name, **arrays):
+    meta = {
+        "torch": torch.__version__,
+        "generator": "tests/golden/make_goldens.py",
+    }
+    arrays = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v))
+              for k, v in arrays.items()}
+    arrays["_meta"] = np.array(repr(meta))
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print(f"{name}: {os.path.getsize(path) / 1024:.0f} KiB")
+
+
+@torch.no_grad()
+def main():
+    torch.set_num_threads(8)
+    ddsp, modules, decoder = import_reference()
+    sr = 48000
+
+    # ---------------- g0: elementwise / layout functions ----------------
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(3, 7, 33, generator=g) * 4.0
+    f0 = 50.0 * 20.0 ** torch.rand(3, 7, 1, generator=g)
+    amps = torch.rand(3, 7, 33, generator=g)
+    up_in = torch.randn(2, 5, 3, generator=g)
+    save("g0_elementwise",
+         scale_in=x, scale_out=ddsp.scale_function(x),
+         nyq_amps=amps, nyq_f0=f0, nyq_out=ddsp.remove_above_nyquist(amps, f0, sr),
+         nyq_out_44k=ddsp.remove_above_nyquist(amps, f0, 44100),
+         up_in=up_in, up_out_3=ddsp.upsample(up_in, 3), up_out_441=ddsp.upsample(up_in, 441))
+
+    # ---------------- g1: harmonic_synth (core.py:136) ----------------
+    # (a) frame-constant controls, small
+    f0, _, param, _ = synth_inputs(0, 2, 8, 16, 65)
+    hs = modules.HarmonicSynth(64, sr)
+    c = hs.get_controls(param[..., :1], param[..., 1:], f0)
+    amp_frames = (c["harmonic_distribution"] * c["amplitudes"]).clone()
+    out = ddsp.harmonic_synth(ddsp.upsample(f0, 64), ddsp.upsample(amp_frames, 64), sr)
+    save("g1_harmonic_small", f0_frames=f0, amp_frames=amp_frames, block_size=64,
+         sample_rate=sr, out=out)
+
+    # (b) per-sample f0 (not frame constant) and per-sample amplitudes
+    g = torch.Generator().manual_seed(11)
+    T = 1000
+    t = torch.arange(T, dtype=torch.float32) / sr
+    f0s = torch.stack([220.0 + 180.0 * torch.sin(2 * np.pi * 3.0 * t),
+                       1500.0 * torch.rand(T, generator=g) + 40.0]).unsqueeze(-1)
+    amps = torch.rand(2, T, 16, generator=g) / 16
+    save("g1_harmonic_persample", f0=f0s, amps=amps, sample_rate=sr,
+         out=ddsp.harmonic_synth(f0s, amps, sr),
+         out_44k=ddsp.harmonic_synth(f0s, amps, 44100))
+
+    # (c) configuration-1 shape: B=1, F=200, bs=512, H=100
+    f0, _, param, _ = synth_inputs(0, 1, 200, 100, 65)
+    hs = modules.HarmonicSynth(512, sr)
+    c = hs.get_controls(param[..., :1], param[..., 1:], f0)
+    out = hs(**c)  # mutates c['harmonic_distribution'] in place (modules.py:73)
+    save("g1_harmonic_full", f0_frames=f0, amp_frames=c["harmonic_distribution"],
+         block_size=512, sample_rate=sr, out=out)
+
+    # (d) configuration-5 harmonic count, long signal: B=1, F=400, H=128 -> |arg| ~ 3e6 rad
+    f0, _, param, _ = synth_inputs(5, 1, 400, 128, 65)
+    f0 = f0.clamp(max=1000.0)
+    hs = modules.HarmonicSynth(512, sr)
+    c = hs.get_controls(param[..., :1], param[..., 1:], f0)
+    out = hs(**c)
+    save("g1_harmonic_h128", f0_frames=f0, amp_frames=c["harmonic_distribution"],
+         block_size=512, sample_rate=sr, out=out)
+
+    # ---------------- g2: HarmonicSynth controls + forward (modules.py:44-80) ----------------
+    f0, _, param, _ = synth_inputs(1, 2, 16, 100, 65)
+    hs = modules.HarmonicSynth(512, sr)
+    c = hs.get_controls(param[..., :1], param[..., 1:], f0)
+    amp_c = c["amplitudes"].clone()
+    dist_c = c["harmonic_distribution"].clone()
+    out = hs(**c)
+    save("g2_controls", param=param, f0=f0, block_size=512, sample_rate=sr,
+         amplitudes=amp_c, distribution=dist_c,
+         distribution_after_forward=c["harmonic_distribution"], out=out)
+    # realtime configuration 3: bs=256, H=64, 4 frames
+    f0, _, param, _ = synth_inputs(3, 1, 4, 64, 65)
+    hs = modules.HarmonicSynth(256, sr)
+    c = hs.get_controls(param[..., :1], param[..., 1:], f0)
+    save("g2_controls_rt", param=param, f0=f0, block_size=256, sample_rate=sr, out=hs(**c))
+
+    # ---------------- g3: FilteredNoise (modules.py:101-128, core.py:144-176) ----------------
+    _, _, _, mags = synth_inputs(2, 2, 16, 100, 65)
+    fn = modules.FilteredNoise(512, 65)
+    nc = fn.get_controls(mags)
+    ir = ddsp.amp_to_impulse_response(nc["magnitudes"], 512)
+    torch.manual_seed(123)
+    noise_in = torch.rand(2, 16, 512) * 2 - 1
+    torch.manual_seed(123)
+    out = fn(**nc)
+    conv = ddsp.fft_convolve(noise_in, ir)
+    assert torch.equal(conv.reshape(2, -1, 1), out)
+    # odd sizes for the function-level boundary
+    g = torch.Generator().manual_seed(12)
+    amp_odd = torch.rand(3, 5, 17, generator=g)
+    sig_odd = torch.randn(4, 100, generator=g)
+    ker_odd = torch.randn(4, 100, generator=g)
+    save("g3_noise", mags=mags, block_size=512, magnitudes=nc["magnitudes"], impulse=ir,
+         noise_in=noise_in, out=out,
+         amp_odd=amp_odd, ir_odd_40=ddsp.amp_to_impulse_response(amp_odd, 40),
+         ir_odd_20=ddsp.amp_to_impulse_response(amp_odd, 20),
+         sig_odd=sig_odd, ker_odd=ker_odd, conv_odd=ddsp.fft_convolve(sig_odd, ker_odd))
+
+    # ---------------- g4: Reverb (modules.py:7-35) ----------------
+    for tag, L, T, B in (("small", 4800, 9600, 2), ("1s", 48000, 102400, 1), ("crop", 48000, 24000, 1)):
+        torch.manual_seed(1)
+        rv = modules.Reverb(L, sr)
+        g = torch.Generator().manual_seed(13)
+        x = torch.randn(B, T, 1, generator=g) * 0.3
+        save(f"g4_reverb_{tag}", length=L, sample_rate=sr, noise=rv.noise, decay=rv.decay,
+             wet=rv.wet, impulse=rv.build_impulse(), x=x, out=rv(x))
+    # non-default wet/decay
+    torch.manual_seed(1)
+    rv = modules.Reverb(4800, sr, initial_wet=1.5, initial_decay=2.0)
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(2, 9600, 1, generator=g) * 0.3
+    save("g4_reverb_wet", length=4800, sample_rate=sr, noise=rv.noise, decay=rv.decay, wet=rv.wet,
+         impulse=rv.build_impulse(), x=x, out=rv(x))
+
+    # ---------------- g5: DDSPDecoder.forward (decoder.py:101) ----------------
+    torch.manual_seed(0)
+    model = decoder.DDSPDecoder(32, 100, 65, sr, 512, True).eval()
+    f0, loudness, _, _ = synth_inputs(4, 1, 16, 100, 65)
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness})
+    sd = {"sd." + k: v for k, v in model.state_dict().items()}
+    save("g5_decoder", hidden_size=32, n_harmonic=100, n_bands=65, sample_rate=sr,
+         block_size=512, pitch=f0, loudness=loudness, signal=o["signal"], noise=o["noise"],
+         harmonic_audio=o["harmonic_audio"],
+         amplitudes=o["harmonic_ctrls"]["amplitudes"],
+         distribution=o["harmonic_ctrls"]["harmonic_distribution"],
+         magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
+
+
+if __name__ == "__main__":
+    main()
