@@ -1,0 +1,90 @@
+"""ctypes binding of the C-ABI library ``lib/libddsp_hip.so`` (declared in include/ddsp_hip.h).
+
+This is the host side of the drop-in boundary: torch supplies device memory and the
+current HIP stream; every entry point is a plain C function taking device pointers,
+sizes and a ``hipStream_t``.  There is no CPU fallback: if the library is missing or a
+tensor is not on a HIP device, the call raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DDSP_HIP_LIB", os.path.join(_HERE, "lib", "libddsp_hip.so"))
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_I = ctypes.c_int
+_U64 = ctypes.c_uint64
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/ddsp_hip.h exactly
+SIGNATURES = {
+    "ddsp_hip_status_string": (ctypes.c_char_p, [_I]),
+    "ddsp_hip_version": (_I, []),
+    "ddsp_hip_scale_function": (_I, [_P, _P, _I64, _F, _P]),
+    "ddsp_hip_remove_above_nyquist": (_I, [_P, _P, _P, _I64, _I64, _F, _P]),
+    "ddsp_hip_upsample": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),
+    "ddsp_hip_harmonic_synth_workspace_size": (_SZ, [_I64, _I64]),
+    "ddsp_hip_harmonic_synth": (_I, [_P, _P, _P, _I64, _I64, _I64, _F, _P, _SZ, _P]),
+    "ddsp_hip_phase": (_I, [_P, _P, _I64, _I64, _F, _P, _SZ, _P]),
+    "ddsp_hip_amp_to_impulse_response": (_I, [_P, _P, _I64, _I64, _I64, _P]),
+    "ddsp_hip_fft_convolve_workspace_size": (_SZ, [_I64, _I64, _I64]),
+    "ddsp_hip_fft_convolve": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_harmonic_controls": (_I, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _F, _P]),
+    "ddsp_hip_harmonic_synth_frames": (_I, [_P, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _F, _P]),
+    "ddsp_hip_filtered_noise": (_I, [_P, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "ddsp_hip_reverb_build_impulse": (_I, [_P, _P, _P, _P, _I64, _F, _P]),
+    "ddsp_hip_reverb_fft_size": (_I64, [_I64, _I64]),
+    "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
+    "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P, _SZ, _P]),
+    "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load (once) and return the C-ABI library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"ddsp_hip: native library not found at {LIB_PATH}; run `make` "
+                    "(or __graft_entry__.build()) — there is no CPU fallback")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    """Invoke ddsp_hip_<name>; map a non-zero status to RuntimeError."""
+    lib = load()
+    st = getattr(lib, "ddsp_hip_" + name)(*args)
+    if st != 0:
+        msg = lib.ddsp_hip_status_string(st).decode()
+        raise RuntimeError(f"ddsp_hip_{name} failed with status {st}: {msg}")
+
+
+def query(name, *args):
+    return getattr(load(), "ddsp_hip_" + name)(*args)
+
+
+def stream_of(t):
+    """The current HIP stream of tensor t's device, as a void*."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

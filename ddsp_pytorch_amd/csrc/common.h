@@ -1,0 +1,116 @@
+// Shared device helpers for the gfx950 DDSP kernels.
+//
+// Numerical contract (checked against the reference's golden
+// vectors by tests/): the reference computes, on CPU in fp32,
+//   inc   = fl32(fl32(fl32(2*pi) * f0) / sr)             ddsp/core.py:138
+//   omega = fl32(sum_{s<=t} (double)inc[s])               torch.cumsum, double accumulator
+//   arg_k = fl32(omega * k)                               ddsp/core.py:139
+//   out   = sum_k sin(arg_k) * A_k                         ddsp/core.py:140
+// Everything here is compiled with -ffp-contract=off: every fused multiply-add is an
+// explicit fmaf(), so no mul->add pair the reference rounds twice is silently fused.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ddsp_hip.h"
+
+namespace ddsp {
+
+constexpr float kTwoPiF = 6.28318548202514648438f;        // fl32(2*pi): ATen casts the scalar
+constexpr float kInvPi = 0.318309886183790671538f;
+constexpr float kPiA = 3.14159274101257324219f;           // fl32(pi)
+constexpr float kPiB = -8.74227765734758577075e-08f;      // fl32(pi - kPiA)
+constexpr float kMagic = 12582912.0f;                     // 1.5 * 2^23: round-to-int shifter
+// |x| below this keeps |x/pi| < 2^22, where the shifter trick yields n exactly and
+// |x - n*pi| <= 1.9 (the polynomial's fitted range).  Larger arguments take the fp64 path.
+constexpr float kFastArgLimit = 1.2e7f;
+
+// Minimax odd polynomial sin(r) = r + r^3 * P(r^2) on |r| <= 1.9 (max error 2e-10;
+// fitted by the repository, not taken from a library).
+constexpr float kS3 = -1.6666666e-01f;
+constexpr float kS5 = 8.3333207e-03f;
+constexpr float kS7 = -1.9839835e-04f;
+constexpr float kS9 = 2.7484100e-06f;
+constexpr float kS11 = -2.3307193e-08f;
+
+// ddsp/core.py:138 — `2 * math.pi * f0 / sample_rate` on fp32 tensors: the python scalar
+// 2*pi is cast to fp32, the product is rounded, then a true (IEEE) fp32 division.
+__device__ __forceinline__ float phase_inc(float f0, float sr) {
+  float p = kTwoPiF * f0;
+  return p / sr;  // correctly rounded (hipcc default: -fhip-fp32-correctly-rounded-divide-sqrt)
+}
+
+// sin of an fp32 argument |x| < kFastArgLimit with abs error <~1.5 ulp(1):
+// n = rint(x/pi) via the shifter (the fma computes x*kInvPi exactly before the single
+// rounding), r = x - n*pi by two fmas (the first is exact: Cody-Waite with an fp32 pi and
+// fma), sin(x) = (-1)^n * sin(r).  15 VALU ops including the caller's x = w*k and acc fma.
+__device__ __forceinline__ float sin_reduced(float x) {
+  float t = fmaf(x, kInvPi, kMagic);
+  float n = t - kMagic;
+  float r = fmaf(-n, kPiA, x);
+  r = fmaf(-n, kPiB, r);
+  float r2 = r * r;
+  float p = fmaf(kS11, r2, kS9);
+  p = fmaf(p, r2, kS7);
+  p = fmaf(p, r2, kS5);
+  p = fmaf(p, r2, kS3);
+  float r3 = r * r2;
+  float s = fmaf(r3, p, r);
+  uint32_t sign = __float_as_uint(t) << 31;  // parity of n sits in the shifter's lsb
+  return __uint_as_float(__float_as_uint(s) ^ sign);
+}
+
+// Arguments beyond kFastArgLimit (long signals at high pitch): fp64 reduction of the
+// exact fp32 value and the fp64 sine, rounded.
+__device__ __noinline__ float sin_slow(float x) { return (float)sin((double)x); }
+
+// Philox4x32-10 (Salmon et al., SC'11): counter-based RNG for the on-device noise.
+struct Philox4 {
+  uint32_t v[4];
+};
+
+__device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                 uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += W0; k1 += W1;
+  }
+  Philox4 r;
+  r.v[0] = c0; r.v[1] = c1; r.v[2] = c2; r.v[3] = c3;
+  return r;
+}
+
+// U[-1, 1) from 24 random bits, the form of `torch.rand(...) * 2 - 1` (modules.py:119-123).
+__device__ __forceinline__ float uniform_pm1(uint32_t bits) {
+  float u = (float)(bits >> 8) * 5.9604644775390625e-08f;  // [0,1) step 2^-24
+  return u * 2.0f - 1.0f;
+}
+
+// Block-wide sum of a double (blockDim.x multiple of 64, <= 1024). Result valid in all threads.
+__device__ __forceinline__ double block_sum_double(double v, double* scratch /*>=16*/) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;
+}
+
+}  // namespace ddsp

@@ -1,0 +1,58 @@
+"""Install the gfx950 path under an imported reference ``ddsp`` package.
+
+Function level: ``ddsp/__init__.py:1`` re-exports ``ddsp.core`` and the synth modules call
+``ddsp.<fn>`` at call time (modules.py:33,53-56,74-78,113,117,125), so rebinding the six
+package attributes redirects every caller.  Module level: the reference classes'
+forwards are replaced by the fused ones (same instance attributes and parameters).
+``uninstall()`` restores everything.
+"""
+from . import core, modules
+
+FUNCTIONS = ("scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
+             "amp_to_impulse_response", "fft_convolve")
+METHODS = {
+    "HarmonicSynth": ("get_controls", "forward"),
+    "FilteredNoise": ("get_controls", "forward", "draw_noise"),
+    "Reverb": ("build_impulse", "forward", "_spectrum"),
+}
+
+
+class Installation:
+    def __init__(self, pkg, saved_fns, saved_methods):
+        self.pkg, self._fns, self._methods = pkg, saved_fns, saved_methods
+
+    def uninstall(self):
+        for name, fn in self._fns.items():
+            setattr(self.pkg, name, fn)
+        for (cls, name), fn in self._methods.items():
+            if fn is None:
+                delattr(cls, name)
+            else:
+                setattr(cls, name, fn)
+        self._fns, self._methods = {}, {}
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.uninstall()
+
+
+def install(pkg=None, functions=True, module_forwards=True):
+    """Redirect the reference package ``pkg`` (default: ``import ddsp``) to the gfx950 kernels."""
+    if pkg is None:
+        import ddsp as pkg  # noqa: the reference package, when importable
+    saved_fns, saved_methods = {}, {}
+    if functions:
+        for name in FUNCTIONS:
+            saved_fns[name] = getattr(pkg, name)
+            setattr(pkg, name, getattr(core, name))
+    if module_forwards:
+        ref_modules = pkg.models.modules
+        for cls_name, names in METHODS.items():
+            ref_cls = getattr(ref_modules, cls_name)
+            ours = getattr(modules, cls_name)
+            for name in names:
+                saved_methods[(ref_cls, name)] = ref_cls.__dict__.get(name)
+                setattr(ref_cls, name, ours.__dict__[name])
+    return Installation(pkg, saved_fns, saved_methods)

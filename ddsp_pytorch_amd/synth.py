@@ -1,0 +1,82 @@
+"""The synthesis section of ``DDSPDecoder.forward`` (decoder.py:106-125) as one fused pipeline:
+frame-rate controls -> harmonic + filtered noise -> reverb -> audio.
+
+This is the unit the benchmark times (SURVEY.md §8(d) "End-to-end unit"): raw
+harmonic parameters [B,F,H+1], pitch [B,F,1] and raw noise magnitudes [B,F,NB] in,
+audio [B,F*bs,1] out.  Kernels per call: harmonic controls, fused oscillator bank,
+noise-magnitude scaling, fused filtered noise (+ harmonic sum), reverb (rocFFT).
+"""
+import torch
+import torch.nn as nn
+
+from . import core
+from .modules import Reverb
+
+
+def make_inputs(batch, frames, n_harmonic, n_bands, block_size, seed=0, device="cpu",
+                with_noise=True):
+    """Seeded synthetic controls of SURVEY.md §8(d): f0 = 50*20**U[0,1) Hz, raw controls
+    N(0,1), noise U[-1,1) from torch.manual_seed(123) (as the reference's torch.rand)."""
+    g = torch.Generator().manual_seed(seed)
+    f0 = 50.0 * 20.0 ** torch.rand(batch, frames, 1, generator=g)
+    loudness = torch.randn(batch, frames, 1, generator=g)
+    param = torch.randn(batch, frames, n_harmonic + 1, generator=g)
+    mags = torch.randn(batch, frames, n_bands, generator=g)
+    out = {"f0": f0, "loudness": loudness, "param": param, "mags": mags}
+    if with_noise:
+        gn = torch.Generator().manual_seed(123 + seed)
+        out["noise"] = torch.rand(batch, frames, block_size, generator=gn) * 2 - 1
+    return {k: v.to(device) for k, v in out.items()}
+
+
+class SynthPath(nn.Module):
+    """Controls -> audio on gfx950.  noise_mode: "inject" (noise tensor given) or "device"."""
+
+    def __init__(self, block_size, sample_rate, reverb_length=None, noise_mode="device",
+                 initial_bias=-5.0, reverb_seed=1):
+        super().__init__()
+        self.block_size = block_size
+        self.sample_rate = sample_rate
+        self.initial_bias = initial_bias
+        self.noise_mode = noise_mode
+        self.reverb = None
+        if reverb_length:
+            state = torch.random.get_rng_state()
+            torch.manual_seed(reverb_seed)  # Reverb built after manual_seed(1)
+            self.reverb = Reverb(reverb_length, sample_rate)
+            torch.random.set_rng_state(state)
+        self.timer = None  # optional callable(name) -> context manager, used by bench.py
+
+    def _t(self, name):
+        if self.timer is None:
+            return _Null()
+        return self.timer(name)
+
+    @torch.no_grad()
+    def forward(self, f0, param, mags, noise=None):
+        with self._t("harmonic_controls"):
+            amps, dist = core.harmonic_controls(param[..., :1], param[..., 1:], f0, self.sample_rate)
+        with self._t("harmonic_synth_frames"):
+            harmonic = core.harmonic_synth_frames(f0, amps, dist, self.block_size, self.sample_rate,
+                                                  write_back=False)
+        with self._t("noise_controls"):
+            m = core.scale_with_bias(mags, self.initial_bias)
+        with self._t("filtered_noise"):
+            if self.noise_mode == "inject":
+                if noise is None:
+                    raise ValueError("noise_mode='inject' needs a noise tensor")
+                signal = core.filtered_noise(m, self.block_size, noise=noise, add=harmonic)
+            else:
+                signal = core.filtered_noise(m, self.block_size, add=harmonic)
+        if self.reverb is not None:
+            with self._t("reverb"):
+                signal = self.reverb(signal)
+        return signal
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

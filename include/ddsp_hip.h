@@ -1,0 +1,138 @@
+/*
+ * ddsp_hip.h — C-ABI of the MI355X (gfx950) DDSP harmonic-plus-noise synthesis path.
+ *
+ * The reference (hugofloresgarcia/ddsp_pytorch) has no native ABI: its hot path is
+ * six module-global Python functions in ddsp/core.py, looked up late-bound through
+ * the `ddsp` package by the synth modules in ddsp/models/modules.py.  Each entry
+ * point below replaces one of those functions (or one module forward) and names
+ * the reference interface it stands in for (file:line under /root/reference).
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers and sizes; fp32 data, contiguous unless a stride is given;
+ *     tensors are channels-last [batch, time, channel] as in the reference;
+ *   - every launch is enqueued on `stream` (a hipStream_t, NULL = default stream);
+ *     nothing synchronises the host;
+ *   - outputs and workspaces are caller-allocated; the library never allocates
+ *     device memory itself (rocFFT plan tables excepted);
+ *   - return DDSP_HIP_OK (0) or a DDSP_HIP_E* code; ddsp_hip_status_string() maps it
+ *     to text.  Invalid shapes are rejected before any launch;
+ *   - thread-safe: callable from any host thread (the rocFFT plan cache is
+ *     mutex-guarded), e.g. the realtime host's worker thread (ddsp_tilde.cpp:88-92).
+ */
+#ifndef DDSP_HIP_H
+#define DDSP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  DDSP_HIP_OK = 0,
+  DDSP_HIP_EINVAL = 1,      /* invalid argument / shape */
+  DDSP_HIP_ELAUNCH = 2,     /* HIP launch or runtime error */
+  DDSP_HIP_EFFT = 3,        /* rocFFT error */
+  DDSP_HIP_EWORKSPACE = 4,  /* workspace too small */
+  DDSP_HIP_ERANGE = 5       /* input outside the exactness domain */
+};
+
+const char* ddsp_hip_status_string(int status);
+int ddsp_hip_version(void);
+
+/* ---------------- function level: ddsp/core.py ---------------- */
+
+/* ddsp/core.py:77-78  scale_function(x) = 2*sigmoid(x)**ln(10) + 1e-7, elementwise over n values.
+ * `bias` is added to x first (FilteredNoise.get_controls, modules.py:111-114 passes -5). */
+int ddsp_hip_scale_function(const float* x, float* y, int64_t n, float bias, void* stream);
+
+/* ddsp/core.py:70-74  remove_above_nyquist(amplitudes[rows,H], f0[rows,1], sr):
+ * out = amps * (fl32(f0*k) < sr/2 ? 1.0001f : 1e-4f), k = 1..H. */
+int ddsp_hip_remove_above_nyquist(const float* amplitudes, const float* f0, float* out,
+                                  int64_t rows, int64_t n_harmonic, float sample_rate,
+                                  void* stream);
+
+/* ddsp/core.py:64-67  upsample(signal[B,F,C], factor) -> [B,F*factor,C] (nearest). */
+int ddsp_hip_upsample(const float* x, float* y, int64_t batch, int64_t frames, int64_t channels,
+                      int64_t factor, void* stream);
+
+/* ddsp/core.py:136-141  harmonic_synth(f0[B,T,1], amplitudes[B,T,H], sr) -> [B,T,1].
+ * Per-sample pitch and amplitudes (the op boundary).  Workspace: see *_workspace_size. */
+size_t ddsp_hip_harmonic_synth_workspace_size(int64_t batch, int64_t n_samples);
+int ddsp_hip_harmonic_synth(const float* f0, const float* amplitudes, float* out, int64_t batch,
+                            int64_t n_samples, int64_t n_harmonic, float sample_rate,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
+/* The fp32 phase omega[B,T] = cumsum(2*pi*f0/sr, time) of ddsp/core.py:138, exposed for
+ * bit-exact testing of the phase accumulator (same code path as harmonic_synth). */
+int ddsp_hip_phase(const float* f0, float* omega, int64_t batch, int64_t n_samples,
+                   float sample_rate, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ddsp/core.py:144-166  amp_to_impulse_response(amp[rows,NB], target) -> [rows,target]. */
+int ddsp_hip_amp_to_impulse_response(const float* amp, float* impulse, int64_t rows,
+                                     int64_t n_bands, int64_t target_size, void* stream);
+
+/* ddsp/core.py:169-176  fft_convolve(signal[rows,N], kernel[kernel_rows,N]) -> [rows,N]:
+ * causal linear convolution truncated to N.  kernel_rows is rows or 1 (broadcast).
+ * Small N runs a direct LDS convolution; large N a rocFFT convolution. */
+size_t ddsp_hip_fft_convolve_workspace_size(int64_t rows, int64_t kernel_rows, int64_t n);
+int ddsp_hip_fft_convolve(const float* signal, const float* kernel, float* out, int64_t rows,
+                          int64_t kernel_rows, int64_t n, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* ---------------- module level: ddsp/models/modules.py ---------------- */
+
+/* modules.py:44-67  HarmonicSynth.get_controls: amplitudes = scale(amp_raw),
+ * dist = remove_above_nyquist(scale(dist_raw), f0, sr) / sum.  Inputs may be strided views
+ * (param[..., :1] and param[..., 1:]): row r of amp_raw is amp_raw[r*amp_stride],
+ * of dist_raw is dist_raw[r*dist_stride + k]. */
+int ddsp_hip_harmonic_controls(const float* amp_raw, int64_t amp_stride, const float* dist_raw,
+                               int64_t dist_stride, const float* f0, float* amplitudes,
+                               float* distribution, int64_t rows, int64_t n_harmonic,
+                               float sample_rate, void* stream);
+
+/* modules.py:69-80  HarmonicSynth.forward fused: dist*amps (written back to `distribution`
+ * in place when write_back != 0, reproducing modules.py:73), frame->sample upsampling of
+ * pitch and amplitudes in registers, and harmonic_synth; [B,F,H] never leaves LDS. */
+int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, float* distribution,
+                                   int write_back, float* out, int64_t batch, int64_t frames,
+                                   int64_t n_harmonic, int64_t block_size, float sample_rate,
+                                   void* stream);
+
+/* modules.py:116-128  FilteredNoise.forward fused: per-frame zero-phase FIR from the
+ * magnitudes (amp_to_impulse_response) applied to block_size noise samples by truncated
+ * linear convolution (fft_convolve).  noise == NULL draws U[-1,1) on device
+ * (Philox4x32-10 keyed by seed, counter offset), else noise[B,F,block_size] is used
+ * (parity mode: the reference's torch.rand stream).  `add` (nullable, [B,F*bs]) is added
+ * to the result (fuses decoder.py:121 `harmonic + noise`); `noise_out` (nullable)
+ * receives the filtered noise alone. */
+int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_t seed,
+                            uint64_t offset, const float* add, float* out, float* noise_out,
+                            int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
+                            void* stream);
+
+/* modules.py:21-26  Reverb.build_impulse: noise[L]*exp(-softplus(-decay)*t*500)*sigmoid(wet),
+ * impulse[0] = 1.  decay and wet are device scalars. */
+int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const float* wet,
+                                  float* impulse, int64_t length, float sample_rate,
+                                  void* stream);
+
+/* modules.py:28-35  Reverb.forward: IR padded/cropped to n_samples, then fft_convolve.
+ * Split in two so the IR spectrum is computed once and cached by the caller:
+ *   ddsp_hip_reverb_spectrum: impulse[L] -> spectrum[(nfft/2+1) complex] (fp32 interleaved),
+ *   ddsp_hip_reverb_apply:   x[B,T] (*) IR -> out[B,T] using that spectrum. */
+int64_t ddsp_hip_reverb_fft_size(int64_t n_samples, int64_t ir_length);
+size_t ddsp_hip_reverb_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length);
+int ddsp_hip_reverb_spectrum(const float* impulse, int64_t ir_length, int64_t n_samples,
+                             float* spectrum, void* workspace, size_t workspace_bytes,
+                             void* stream);
+int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int64_t batch,
+                          int64_t n_samples, int64_t ir_length, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DDSP_HIP_H */

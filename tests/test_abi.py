@@ -1,0 +1,76 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds, loads and exports every
+symbol include/ddsp_hip.h declares (no compute: there is no GPU here), and the host layer
+refuses CPU tensors instead of falling back."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ddsp_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(ddsp_hip_\w+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "ddsp_hip_harmonic_synth" in syms and "ddsp_hip_filtered_noise" in syms
+    assert len(syms) >= 19
+
+
+def test_library_exports_every_declared_symbol():
+    from ddsp_pytorch_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-C", ROOT, "-j4"], check=True)
+    lib = _lib.load()
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r"\b(ddsp_hip_\w+)\b", nm))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    # the ctypes table binds exactly the declared set
+    assert set(_lib.SIGNATURES) == set(declared_symbols())
+    assert lib.ddsp_hip_version() >= 100
+    assert lib.ddsp_hip_status_string(1) == b"invalid argument or shape"
+
+
+def test_abi_rejects_bad_arguments_without_launching():
+    from ddsp_pytorch_amd import _lib
+    lib = _lib.load()
+    import ctypes
+    null = ctypes.c_void_p(0)
+    # negative sizes / missing buffers are rejected before any HIP call
+    assert lib.ddsp_hip_scale_function(null, null, -1, 0.0, null) == 1
+    assert lib.ddsp_hip_upsample(null, null, 1, 1, 1, 0, null) == 1
+    assert lib.ddsp_hip_harmonic_synth(null, null, null, 1, 10, 4, 48000.0, null, 0, null) == 1
+    assert lib.ddsp_hip_filtered_noise(null, null, 0, 0, null, null, null, 1, 1, 1, 512, null) == 1
+    assert lib.ddsp_hip_fft_convolve(null, null, null, 4, 3, 100, null, 0, null) == 1
+    # empty inputs are a no-op success
+    assert lib.ddsp_hip_scale_function(null, null, 0, 0.0, null) == 0
+    assert lib.ddsp_hip_harmonic_synth_frames(null, null, null, 0, null, 0, 5, 4, 512, 48000.0, null) == 0
+
+
+def test_no_cpu_fallback():
+    import ddsp_pytorch_amd as dd
+    x = torch.zeros(1, 4, 3)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        dd.core.scale_function(x)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        dd.core.harmonic_synth(torch.zeros(1, 8, 1), torch.zeros(1, 8, 4), 48000)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        dd.HarmonicSynth(512, 48000).get_controls(x[..., :1], x, x[..., :1])
+
+
+def test_module_state_dict_keys_match_reference_layout():
+    import ddsp_pytorch_amd as dd
+    m = dd.DDSPDecoder(32, 100, 65, 48000, 512, True)
+    keys = set(m.state_dict())
+    for k in ("sample_rate", "block_size", "phase", "decoder.cache_gru", "decoder.gru.weight_ih_l0",
+              "decoder.f0_mlp.0.weight", "decoder.out_mlp.7.bias", "harmonic_proj.weight",
+              "noise_proj.bias", "reverb.noise", "reverb.decay", "reverb.wet", "reverb.t"):
+        assert k in keys, k
