@@ -1,15 +1,21 @@
 # Builds the gfx950 C-ABI library ddsp_pytorch_amd/lib/libddsp_hip.so (hipcc cross-compiles
-# without a GPU) and the C oracle used by tests.
+# without a GPU).
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-SRC := ddsp_pytorch_amd/csrc/synth.hip ddsp_pytorch_amd/csrc/noise.hip ddsp_pytorch_amd/csrc/reverb.hip
-HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h
+SRC := ddsp_pytorch_amd/csrc/synth.hip ddsp_pytorch_amd/csrc/noise.hip ddsp_pytorch_amd/csrc/reverb.hip \
+       ddsp_pytorch_amd/csrc/upols.hip
+HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h ddsp_pytorch_amd/csrc/upols.h
 LIB := ddsp_pytorch_amd/lib/libddsp_hip.so
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Wall \
-            -Wno-unused-result -munsafe-fp-atomics
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ibuild -Wall -Wno-unused-result
 OBJ := $(patsubst ddsp_pytorch_amd/csrc/%.hip,build/%.o,$(SRC))
 
 all: $(LIB)
+
+build/twiddle4096.inc: tools/gen_twiddles.py
+	@mkdir -p build
+	python3 tools/gen_twiddles.py 4096 > $@
+
+build/upols.o: build/twiddle4096.inc
 
 build/%.o: ddsp_pytorch_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
@@ -17,7 +23,7 @@ build/%.o: ddsp_pytorch_amd/csrc/%.hip $(HDR)
 
 $(LIB): $(OBJ)
 	@mkdir -p ddsp_pytorch_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
 
 clean:
 	rm -rf build $(LIB)

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
-    "harmonic_synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_fft_size",
+    "harmonic_synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
     "reverb_spectrum", "reverb_apply", "set_noise_seed",
 ]
 
@@ -300,20 +300,17 @@ def reverb_build_impulse(noise, decay, wet, sample_rate):
     return imp
 
 
-def reverb_fft_size(n_samples, ir_length):
-    return int(_lib.query("reverb_fft_size", int(n_samples), int(ir_length)))
+def reverb_spectrum_floats(n_samples, ir_length):
+    return int(_lib.query("reverb_spectrum_floats", int(n_samples), int(ir_length)))
 
 
 def reverb_spectrum(impulse, n_samples):
-    """Spectrum of the IR cropped/padded to n_samples, at the FFT size reverb_apply uses."""
+    """Partitioned-convolution spectra of the IR cropped/padded to n_samples (for reverb_apply)."""
     _dev(impulse)
     h = _c(impulse.reshape(-1))
     L = h.numel()
-    nfft = reverb_fft_size(n_samples, L)
-    spec = torch.empty(nfft + 2, dtype=torch.float32, device=h.device)
-    ws = _workspace(_lib.query("reverb_workspace_size", 1, int(n_samples), L), h.device)
-    _lib.call("reverb_spectrum", _lib.ptr(h), L, int(n_samples), _lib.ptr(spec), _lib.ptr(ws),
-              ws.numel(), _lib.stream_of(h))
+    spec = torch.empty(reverb_spectrum_floats(n_samples, L), dtype=torch.float32, device=h.device)
+    _lib.call("reverb_spectrum", _lib.ptr(h), L, int(n_samples), _lib.ptr(spec), _lib.stream_of(h))
     return spec
 
 
@@ -322,7 +319,7 @@ def reverb_apply(x, spectrum, ir_length):
     _dev(x, spectrum)
     _no_grad_guard(x)
     B, T = x.shape[0], x.shape[1]
-    if spectrum.numel() != reverb_fft_size(T, ir_length) + 2:
+    if spectrum.numel() != reverb_spectrum_floats(T, ir_length):
         raise RuntimeError("reverb_apply: spectrum was computed for a different length")
     xc = _c(x)
     out = torch.empty(B, T, 1, dtype=torch.float32, device=x.device)

@@ -288,6 +288,92 @@ __global__ void __launch_bounds__(kScanNT) harmonic_samples_kernel(
   }
 }
 
+// Tiled op-boundary kernel (H % 4 == 0, H <= 128): the [64 samples x H] amplitude tile of
+// each stage is contiguous in HBM, so it is streamed with fully coalesced 16-byte loads into
+// LDS (register-staged one stage ahead, overlapping the sines of the current stage), then
+// 4 lanes share a sample, each summing every 4th harmonic.  LDS rows are padded to a stride
+// == 4 (mod 8) floats so the 32 lanes of a half-wave (8 samples x 4 lanes) hit 32 banks.
+constexpr int kStage = 64;      // samples per stage
+constexpr int kTileMaxPF = 8;   // float4 per thread per stage: 64*H/4/256 = H/16 <= 8
+__global__ void __launch_bounds__(kScanNT) harmonic_samples_tiled_kernel(
+    const float* __restrict__ f0, const float* __restrict__ amps, const double* __restrict__ sums,
+    float* __restrict__ out, int64_t T, int nchunks, int H, int Hs, float sr) {
+  extern __shared__ float4 tile4[];
+  float* tile = reinterpret_cast<float*>(tile4);  // [kStage][Hs]
+  __shared__ float wsm[kChunk];
+  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  {
+    float w[kScanSPT];
+    chunk_phase(f0 + (int64_t)b * T, sums + (int64_t)b * nchunks, T, c, sr, w);
+#pragma unroll
+    for (int s = 0; s < kScanSPT; ++s) wsm[tid * kScanSPT + s] = w[s];
+  }
+  const int64_t chunk_t0 = (int64_t)c * kChunk;
+  const int valid = (int)min<int64_t>(kChunk, T - chunk_t0);
+  const int nstage = (valid + kStage - 1) / kStage;
+  const int H4 = H >> 2;
+  const float invH4 = 1.0f / (float)H4;
+  const float4* src = reinterpret_cast<const float4*>(amps + ((int64_t)b * T + chunk_t0) * H);
+
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f pre[kTileMaxPF];
+  auto prefetch = [&](int st) {
+    const int rows = min(kStage, valid - st * kStage);
+    const int n4 = rows * H4;
+    const v4f* s4 = reinterpret_cast<const v4f*>(src) + (int64_t)st * kStage * H4;
+#pragma unroll
+    for (int i = 0; i < kTileMaxPF; ++i) {
+      const int e = tid + i * kScanNT;
+      if (e < n4) pre[i] = __builtin_nontemporal_load(s4 + e);
+    }
+  };
+  auto commit = [&](int st) {
+    const int rows = min(kStage, valid - st * kStage);
+    const int n4 = rows * H4;
+#pragma unroll
+    for (int i = 0; i < kTileMaxPF; ++i) {
+      const int e = tid + i * kScanNT;
+      if (e < n4) {
+        int row = (int)(((float)e + 0.5f) * invH4);
+        const int col4 = e - row * H4;
+        *reinterpret_cast<v4f*>(tile + row * Hs + 4 * col4) = pre[i];
+      }
+    }
+  };
+
+  const int sl = tid >> 2, q = tid & 3;
+  if (nstage > 0) prefetch(0);
+  for (int st = 0; st < nstage; ++st) {
+    __syncthreads();  // previous stage's reads done (and wsm visible on the first pass)
+    commit(st);
+    __syncthreads();
+    if (st + 1 < nstage) prefetch(st + 1);
+    const int i = st * kStage + sl;
+    const float w = wsm[i < kChunk ? i : 0];
+    const float* arow = tile + sl * Hs;
+    float acc0 = 0.0f, acc1 = 0.0f;
+    if (fabsf(w) * (float)H < kFastArgLimit) {
+      for (int k = q; k < H; k += 16) {
+        // k, k+4, k+8, k+12 (H % 4 == 0 keeps k+4j < H whenever k < H - 12; guard the tail)
+        acc0 = fmaf(sin_reduced(w * (float)(k + 1)), arow[k], acc0);
+        if (k + 4 < H) acc1 = fmaf(sin_reduced(w * (float)(k + 5)), arow[k + 4], acc1);
+        if (k + 8 < H) acc0 = fmaf(sin_reduced(w * (float)(k + 9)), arow[k + 8], acc0);
+        if (k + 12 < H) acc1 = fmaf(sin_reduced(w * (float)(k + 13)), arow[k + 12], acc1);
+      }
+    } else {
+      for (int k = q; k < H; k += 4) {
+        const float x = w * (float)(k + 1);
+        const float sn = fabsf(x) < kFastArgLimit ? sin_reduced(x) : sin_slow(x);
+        acc0 = fmaf(sn, arow[k], acc0);
+      }
+    }
+    float acc = acc0 + acc1;
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (q == 0 && i < valid) out[(int64_t)b * T + chunk_t0 + i] = acc;
+  }
+}
+
 inline unsigned grid1d(int64_t n, int nt) {
   int64_t g = (n + nt - 1) / nt;
   return (unsigned)std::min<int64_t>(std::max<int64_t>(g, 1), 65536);
@@ -410,7 +496,15 @@ int ddsp_hip_harmonic_synth(const float* f0, const float* amplitudes, float* out
   int st = phase_common(f0, batch, n_samples, sample_rate, workspace, workspace_bytes, stream, &nchunks);
   if (st) return st;
   const bool vec4 = (n_harmonic % 4 == 0) && ((reinterpret_cast<uintptr_t>(amplitudes) & 15) == 0);
-  if (vec4)
+  if (vec4 && n_harmonic <= 4 * kTileMaxPF * kScanNT / kStage) {
+    const int H = (int)n_harmonic;
+    const int Hs = H + ((12 - (H & 7)) & 7);  // smallest stride >= H with stride == 4 (mod 8)
+    const size_t shm = sizeof(float) * (size_t)kStage * Hs;
+    hipLaunchKernelGGL(harmonic_samples_tiled_kernel, dim3((unsigned)nchunks, (unsigned)batch),
+                       dim3(kScanNT), shm, S(stream), f0, amplitudes,
+                       reinterpret_cast<const double*>(workspace), out, n_samples, nchunks, H, Hs,
+                       sample_rate);
+  } else if (vec4)
     hipLaunchKernelGGL(harmonic_samples_kernel<true>, dim3((unsigned)nchunks, (unsigned)batch),
                        dim3(kScanNT), 0, S(stream), f0, amplitudes,
                        reinterpret_cast<const double*>(workspace), out, n_samples, nchunks,

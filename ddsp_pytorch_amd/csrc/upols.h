@@ -1,0 +1,21 @@
+// Uniformly partitioned overlap-save convolution (upols.hip): internal API of the library.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ddsp {
+constexpr int kP = 2048;  // partition (block) length
+constexpr int kN = 4096;  // FFT length
+
+int64_t upols_partitions(int64_t klen);
+int64_t upols_blocks(int64_t n);
+size_t upols_spectrum_floats(int64_t krows, int64_t klen);
+size_t upols_workspace_bytes(int64_t rows, int64_t n, bool pairing);
+// spectra of krows kernels (row stride ld, first klen taps used), scaled by 1/N
+int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, float* spectrum,
+                   void* stream);
+// y[rows, n] = (x[rows, n] (*) h)[0:n]; spectrum from upols_spectrum (one kernel shared by all
+// rows, or one per row when per_row_kernel).  klen = kernel length the spectrum was made with.
+int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
+                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream);
+}  // namespace ddsp

@@ -1,0 +1,284 @@
+// Uniformly partitioned overlap-save (UPOLS) FFT convolution for gfx950.
+//
+// Replaces the reference's one-shot 2T-point FFT convolution (ddsp/core.py:169-176, used by
+// Reverb.forward, ddsp/models/modules.py:28-35) for long signals and kernels.  Only the first
+// T outputs of the causal linear convolution are kept, so any exact method is a faithful
+// restatement; this one is laid out for the MI355X memory system:
+//
+//   partition size P = 2048, FFT size N = 4096 (= 16^3: three radix-16 Stockham passes, one
+//   workgroup of 256 threads per transform, 16 points per thread, 34 KB of LDS);
+//   two real rows sharing one kernel are packed as z = x_a + i*x_b: the kernel is real, so
+//   z (*) h = (x_a (*) h) + i (x_b (*) h) — one complex FFT serves two rows with no
+//   Hermitian post-processing;
+//   kernel partitions h_p = h[pP, (p+1)P) -> H_p = FFT_N([h_p, 0]) / N   (computed once);
+//   forward:  X_b = FFT_N(z[(b-1)P, (b+1)P))                 (upols_forward_kernel)
+//   MAC:      Y_b = sum_p X_{b-p} H_p   per frequency bin     (upols_mac_kernel)
+//   inverse:  y[bP, (b+1)P) = last P points of IFFT_N(Y_b)    (upols_inverse_kernel)
+//
+// HBM traffic per real output sample: x read twice (overlap, 8 B), X write/read (16 B),
+// Y write/read (16 B), y write (4 B).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "upols.h"
+#include "twiddle4096.inc"
+
+namespace ddsp {
+namespace {
+
+constexpr int kNT = 256;            // threads per transform
+constexpr int kPad = kN + kN / 16;  // LDS float2 slots: one pad slot per 16 (bank spreading)
+
+__device__ __forceinline__ int lds_idx(int i) { return i + (i >> 4); }
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+
+__device__ __forceinline__ float2 twiddle(int m, bool inv) {
+  const float2 w = reinterpret_cast<const float2*>(kTwiddle4096)[m];
+  return inv ? make_float2(w.x, -w.y) : w;
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
+  const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
+  const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
+  const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
+  // forward: W4 = -i ; inverse: +i.  (-i)*(x+iy) = y - ix
+  const float2 rot = INV ? make_float2(-d13.y, d13.x) : make_float2(d13.y, -d13.x);
+  a0 = make_float2(s02.x + s13.x, s02.y + s13.y);
+  a2 = make_float2(s02.x - s13.x, s02.y - s13.y);
+  a1 = make_float2(d02.x + rot.x, d02.y + rot.y);
+  a3 = make_float2(d02.x - rot.x, d02.y - rot.y);
+}
+
+// 16-point DFT in registers: r = 4 r1 + r0, k = k0 + 4 k1.
+template <bool INV>
+__device__ __forceinline__ void dft16(float2 (&v)[16]) {
+#pragma unroll
+  for (int r0 = 0; r0 < 4; ++r0) dft4<INV>(v[r0], v[4 + r0], v[8 + r0], v[12 + r0]);
+  // v[4*k0 + r0] now holds u[r0][k0]; internal twiddles W16^{r0*k0} = W4096^{256*r0*k0}
+#pragma unroll
+  for (int r0 = 1; r0 < 4; ++r0)
+#pragma unroll
+    for (int k0 = 1; k0 < 4; ++k0) v[4 * k0 + r0] = cmul(v[4 * k0 + r0], twiddle(256 * r0 * k0, INV));
+  float2 t[16];
+#pragma unroll
+  for (int k0 = 0; k0 < 4; ++k0) {
+    float2 a0 = v[4 * k0 + 0], a1 = v[4 * k0 + 1], a2 = v[4 * k0 + 2], a3 = v[4 * k0 + 3];
+    dft4<INV>(a0, a1, a2, a3);
+    t[k0 + 0] = a0; t[k0 + 4] = a1; t[k0 + 8] = a2; t[k0 + 12] = a3;  // X[k0 + 4 k1]
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
+// One Stockham radix-16 pass on registers v (inputs in[j + 256 r]): twiddle, DFT16.
+// Output element r goes to index ((j/Ns)*Ns*16 + j%Ns) + r*Ns.
+template <bool INV>
+__device__ __forceinline__ void pass(float2 (&v)[16], int j, int Ns) {
+  const int k = j & (Ns - 1);
+  if (Ns > 1) {
+    const int step = k * (kN / (Ns * 16));
+#pragma unroll
+    for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], twiddle(r * step, INV));
+  }
+  dft16<INV>(v);
+}
+
+__device__ __forceinline__ int out_index(int j, int Ns, int r) {
+  return (j / Ns) * Ns * 16 + (j & (Ns - 1)) + r * Ns;
+}
+
+// Full 4096-point transform: v holds in[j + 256 r] on entry and out[j + 256 r] on exit.
+template <bool INV>
+__device__ __forceinline__ void fft4096(float2 (&v)[16], float2* lds) {
+  const int j = threadIdx.x;
+  pass<INV>(v, j, 1);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[lds_idx(out_index(j, 1, r))] = v[r];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = lds[lds_idx(j + 256 * r)];
+  __syncthreads();
+  pass<INV>(v, j, 16);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[lds_idx(out_index(j, 16, r))] = v[r];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = lds[lds_idx(j + 256 * r)];
+  pass<INV>(v, j, 256);  // Ns = 256: output index == j + 256 r (coalesced)
+}
+
+// rows of the packed signal: pair -> (row_a, row_b or -1)
+__device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
+  if (pairing) {
+    ra = 2 * pair;
+    rb = 2 * pair + 1 < rows ? 2 * pair + 1 : -1;
+  } else {
+    ra = pair;
+    rb = -1;
+  }
+}
+
+// X[pair][b][:] = FFT(z[(b-1)P, (b+1)P)); grid (nb, npairs)
+__global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
+                                                            int64_t T, int rows, int pairing, int nb,
+                                                            float2* __restrict__ X) {
+  __shared__ float2 lds[kPad];
+  const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
+  int ra, rb;
+  pair_rows(pair, rows, pairing, ra, rb);
+  const float* xa = x + (int64_t)ra * ld;
+  const float* xb = rb >= 0 ? x + (int64_t)rb * ld : nullptr;
+  const int64_t s0 = (int64_t)(b - 1) * kP;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = s0 + j + 256 * r;
+    const bool ok = s >= 0 && s < T;
+    v[r] = make_float2(ok ? xa[s] : 0.0f, (ok && xb) ? xb[s] : 0.0f);
+  }
+  fft4096<false>(v, lds);
+  float2* out = X + ((int64_t)pair * nb + b) * kN;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+}
+
+// H[row][p][:] = FFT([h[row][pP, pP+P) (within klen), 0]) / N; grid (Q, krows)
+__global__ void __launch_bounds__(kNT) upols_kernel_spectrum_kernel(const float* __restrict__ h,
+                                                                    int64_t ld, int64_t klen, int Q,
+                                                                    float2* __restrict__ Hs) {
+  __shared__ float2 lds[kPad];
+  const int p = blockIdx.x, row = blockIdx.y, j = threadIdx.x;
+  const float* hr = h + (int64_t)row * ld;
+  const float inv_n = 1.0f / (float)kN;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = j + 256 * r;
+    const int64_t s = (int64_t)p * kP + n;
+    v[r] = make_float2((n < kP && s < klen) ? hr[s] * inv_n : 0.0f, 0.0f);
+  }
+  fft4096<false>(v, lds);
+  float2* out = Hs + ((int64_t)row * Q + p) * kN;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+}
+
+// Y[pair][b][f] = sum_p X[pair][b-p][f] * H[p][f]; each thread one bin, 8 consecutive blocks.
+// grid (N/256, ceil(nb/8), npairs)
+constexpr int kMacBlk = 8;
+__global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict__ X,
+                                                        const float2* __restrict__ Hs,
+                                                        int64_t h_pair_stride, int nb, int Q,
+                                                        float2* __restrict__ Y) {
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int b0 = blockIdx.y * kMacBlk;
+  const int pair = blockIdx.z;
+  const float2* Xp = X + (int64_t)pair * nb * kN + f;
+  const float2* Hp = Hs + (int64_t)pair * h_pair_stride + f;
+  float2 acc[kMacBlk], win[kMacBlk];
+#pragma unroll
+  for (int d = 0; d < kMacBlk; ++d) {
+    acc[d] = make_float2(0.f, 0.f);
+    win[d] = (b0 + d < nb) ? Xp[(int64_t)(b0 + d) * kN] : make_float2(0.f, 0.f);
+  }
+  const int pmax = min(Q, b0 + kMacBlk);
+  for (int p = 0; p < pmax; ++p) {
+    const float2 h = Hp[(int64_t)p * kN];
+#pragma unroll
+    for (int d = 0; d < kMacBlk; ++d) {
+      acc[d].x = fmaf(win[d].x, h.x, fmaf(-win[d].y, h.y, acc[d].x));
+      acc[d].y = fmaf(win[d].x, h.y, fmaf(win[d].y, h.x, acc[d].y));
+    }
+#pragma unroll
+    for (int d = kMacBlk - 1; d > 0; --d) win[d] = win[d - 1];
+    const int bn = b0 - p - 1;
+    win[0] = bn >= 0 ? Xp[(int64_t)bn * kN] : make_float2(0.f, 0.f);
+  }
+  float2* Yp = Y + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int d = 0; d < kMacBlk; ++d)
+    if (b0 + d < nb) Yp[(int64_t)(b0 + d) * kN] = acc[d];
+}
+
+// y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
+__global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __restrict__ Y, int nb,
+                                                            int64_t T, int rows, int pairing,
+                                                            float* __restrict__ y, int64_t ld) {
+  __shared__ float2 lds[kPad];
+  const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
+  const float2* in = Y + ((int64_t)pair * nb + b) * kN;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = in[j + 256 * r];
+  fft4096<true>(v, lds);
+  int ra, rb;
+  pair_rows(pair, rows, pairing, ra, rb);
+  float* ya = y + (int64_t)ra * ld;
+  float* yb = rb >= 0 ? y + (int64_t)rb * ld : nullptr;
+#pragma unroll
+  for (int r = 8; r < 16; ++r) {
+    const int64_t s = (int64_t)b * kP + j + 256 * r - kP;
+    if (s < T) {
+      ya[s] = v[r].x;
+      if (yb) yb[s] = v[r].y;
+    }
+  }
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+int64_t upols_partitions(int64_t klen) { return (std::max<int64_t>(klen, 1) + kP - 1) / kP; }
+int64_t upols_blocks(int64_t n) { return (n + kP - 1) / kP; }
+
+size_t upols_spectrum_floats(int64_t krows, int64_t klen) {
+  return (size_t)krows * (size_t)upols_partitions(klen) * kN * 2;
+}
+
+size_t upols_workspace_bytes(int64_t rows, int64_t n, bool pairing) {
+  const int64_t npairs = pairing ? (rows + 1) / 2 : rows;
+  return 2 * (size_t)npairs * (size_t)upols_blocks(n) * kN * sizeof(float2);
+}
+
+int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, float* spectrum,
+                   void* stream) {
+  const int64_t Q = upols_partitions(klen);
+  if (Q > 65535 || krows > 65535) return DDSP_HIP_EINVAL;
+  hipLaunchKernelGGL(upols_kernel_spectrum_kernel, dim3((unsigned)Q, (unsigned)krows), dim3(kNT), 0,
+                     S(stream), h, ld, klen, (int)Q, reinterpret_cast<float2*>(spectrum));
+  return launch_status();
+}
+
+int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
+                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream) {
+  const bool pairing = !per_row_kernel;
+  const int64_t npairs = pairing ? (rows + 1) / 2 : rows;
+  const int64_t nb = upols_blocks(n);
+  const int64_t Q = upols_partitions(std::min(klen, n));
+  if (!ws || ws_bytes < upols_workspace_bytes(rows, n, pairing)) return DDSP_HIP_EWORKSPACE;
+  if (nb > INT32_MAX || npairs > 65535 || (nb + kMacBlk - 1) / kMacBlk > 65535) return DDSP_HIP_EINVAL;
+  float2* X = reinterpret_cast<float2*>(ws);
+  float2* Y = X + (size_t)npairs * nb * kN;
+  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
+                     x, n, n, (int)rows, (int)pairing, (int)nb, X);
+  int st = launch_status();
+  if (st) return st;
+  const int64_t h_stride = per_row_kernel ? upols_partitions(klen) * kN : 0;
+  hipLaunchKernelGGL(upols_mac_kernel, dim3(kN / kNT, (unsigned)((nb + kMacBlk - 1) / kMacBlk), (unsigned)npairs),
+                     dim3(kNT), 0, S(stream), X, reinterpret_cast<const float2*>(spectrum), h_stride,
+                     (int)nb, (int)Q, Y);
+  if ((st = launch_status())) return st;
+  hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
+                     Y, (int)nb, n, (int)rows, (int)pairing, y, n);
+  return launch_status();
+}
+
+}  // namespace ddsp

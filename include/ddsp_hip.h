@@ -13,11 +13,11 @@
  *   - every launch is enqueued on `stream` (a hipStream_t, NULL = default stream);
  *     nothing synchronises the host;
  *   - outputs and workspaces are caller-allocated; the library never allocates
- *     device memory itself (rocFFT plan tables excepted);
+ *     device memory;
  *   - return DDSP_HIP_OK (0) or a DDSP_HIP_E* code; ddsp_hip_status_string() maps it
  *     to text.  Invalid shapes are rejected before any launch;
- *   - thread-safe: callable from any host thread (the rocFFT plan cache is
- *     mutex-guarded), e.g. the realtime host's worker thread (ddsp_tilde.cpp:88-92).
+ *   - thread-safe and stateless: callable from any host thread, e.g. the realtime
+ *     host's worker thread (ddsp_tilde.cpp:88-92).
  */
 #ifndef DDSP_HIP_H
 #define DDSP_HIP_H
@@ -33,7 +33,7 @@ enum {
   DDSP_HIP_OK = 0,
   DDSP_HIP_EINVAL = 1,      /* invalid argument / shape */
   DDSP_HIP_ELAUNCH = 2,     /* HIP launch or runtime error */
-  DDSP_HIP_EFFT = 3,        /* rocFFT error */
+  DDSP_HIP_EFFT = 3,        /* FFT convolution error */
   DDSP_HIP_EWORKSPACE = 4,  /* workspace too small */
   DDSP_HIP_ERANGE = 5       /* input outside the exactness domain */
 };
@@ -75,7 +75,7 @@ int ddsp_hip_amp_to_impulse_response(const float* amp, float* impulse, int64_t r
 
 /* ddsp/core.py:169-176  fft_convolve(signal[rows,N], kernel[kernel_rows,N]) -> [rows,N]:
  * causal linear convolution truncated to N.  kernel_rows is rows or 1 (broadcast).
- * Small N runs a direct LDS convolution; large N a rocFFT convolution. */
+ * Small N runs a direct LDS convolution; large N a partitioned overlap-save FFT convolution. */
 size_t ddsp_hip_fft_convolve_workspace_size(int64_t rows, int64_t kernel_rows, int64_t n);
 int ddsp_hip_fft_convolve(const float* signal, const float* kernel, float* out, int64_t rows,
                           int64_t kernel_rows, int64_t n, void* workspace,
@@ -120,13 +120,13 @@ int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const 
 
 /* modules.py:28-35  Reverb.forward: IR padded/cropped to n_samples, then fft_convolve.
  * Split in two so the IR spectrum is computed once and cached by the caller:
- *   ddsp_hip_reverb_spectrum: impulse[L] -> spectrum[(nfft/2+1) complex] (fp32 interleaved),
+ *   ddsp_hip_reverb_spectrum: impulse[L] -> spectrum (ddsp_hip_reverb_spectrum_floats floats:
+ *     partitioned-convolution spectra of the IR cropped to min(L, n_samples));
  *   ddsp_hip_reverb_apply:   x[B,T] (*) IR -> out[B,T] using that spectrum. */
-int64_t ddsp_hip_reverb_fft_size(int64_t n_samples, int64_t ir_length);
+size_t ddsp_hip_reverb_spectrum_floats(int64_t n_samples, int64_t ir_length);
 size_t ddsp_hip_reverb_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length);
 int ddsp_hip_reverb_spectrum(const float* impulse, int64_t ir_length, int64_t n_samples,
-                             float* spectrum, void* workspace, size_t workspace_bytes,
-                             void* stream);
+                             float* spectrum, void* stream);
 int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int64_t batch,
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
