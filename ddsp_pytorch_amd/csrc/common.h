@@ -22,17 +22,17 @@ constexpr float kInvPi = 0.318309886183790671538f;
 constexpr float kPiA = 3.14159274101257324219f;           // fl32(pi)
 constexpr float kPiB = -8.74227765734758577075e-08f;      // fl32(pi - kPiA)
 constexpr float kMagic = 12582912.0f;                     // 1.5 * 2^23: round-to-int shifter
-// |x| below this keeps |x/pi| < 2^22, where the shifter trick yields n exactly and
-// |x - n*pi| <= 1.9 (the polynomial's fitted range).  Larger arguments take the fp64 path.
-constexpr float kFastArgLimit = 1.2e7f;
+// |x| below this keeps |x/pi| < 2^22 (the shifter yields n exactly) and, given the 1.28e-8
+// representation error of kInvPi, |x - n*pi| <= 1.9, the polynomial's fitted range.
+// Larger arguments take the fp64 path.
+constexpr float kFastArgLimit = 8.0e6f;
 
-// Minimax odd polynomial sin(r) = r + r^3 * P(r^2) on |r| <= 1.9 (max error 2e-10;
-// fitted by the repository, not taken from a library).
-constexpr float kS3 = -1.6666666e-01f;
-constexpr float kS5 = 8.3333207e-03f;
-constexpr float kS7 = -1.9839835e-04f;
-constexpr float kS9 = 2.7484100e-06f;
-constexpr float kS11 = -2.3307193e-08f;
+// Minimax odd polynomial sin(r) = r * (1 + r^2 * P(r^2)), P of degree 3, on |r| <= 1.9
+// (max approximation error 3.7e-8; fitted by the repository, not taken from a library).
+constexpr float kS3 = -0.16666624f;
+constexpr float kS5 = 0.008332362f;
+constexpr float kS7 = -0.00019768332f;
+constexpr float kS9 = 2.5307909e-06f;
 
 // ddsp/core.py:138 — `2 * math.pi * f0 / sample_rate` on fp32 tensors: the python scalar
 // 2*pi is cast to fp32, the product is rounded, then a true (IEEE) fp32 division.
@@ -41,24 +41,41 @@ __device__ __forceinline__ float phase_inc(float f0, float sr) {
   return p / sr;  // correctly rounded (hipcc default: -fhip-fp32-correctly-rounded-divide-sqrt)
 }
 
-// sin of an fp32 argument |x| < kFastArgLimit with abs error <~1.5 ulp(1):
-// n = rint(x/pi) via the shifter (the fma computes x*kInvPi exactly before the single
-// rounding), r = x - n*pi by two fmas (the first is exact: Cody-Waite with an fp32 pi and
-// fma), sin(x) = (-1)^n * sin(r).  15 VALU ops including the caller's x = w*k and acc fma.
-__device__ __forceinline__ float sin_reduced(float x) {
-  float t = fmaf(x, kInvPi, kMagic);
-  float n = t - kMagic;
+// Reduced argument with the sign of (-1)^n folded in: sin(x) = sin(rs) for |x| < kFastArgLimit.
+// n = rint(x/pi) via the shifter (the fma forms x*kInvPi exactly before its single rounding),
+// r = x - n*pi by two fmas (the first exact: Cody-Waite with an fp32 pi and fma); the parity
+// of n — the shifter's lsb — is moved into r's sign bit by one integer shift-and-add
+// (adding 2^31 toggles bit 31).  5 VALU ops.
+__device__ __forceinline__ float reduce_signed(float x) {
+  const float t = fmaf(x, kInvPi, kMagic);
+  const float n = t - kMagic;
   float r = fmaf(-n, kPiA, x);
   r = fmaf(-n, kPiB, r);
-  float r2 = r * r;
-  float p = fmaf(kS11, r2, kS9);
-  p = fmaf(p, r2, kS7);
-  p = fmaf(p, r2, kS5);
-  p = fmaf(p, r2, kS3);
-  float r3 = r * r2;
-  float s = fmaf(r3, p, r);
-  uint32_t sign = __float_as_uint(t) << 31;  // parity of n sits in the shifter's lsb
-  return __uint_as_float(__float_as_uint(s) ^ sign);
+  return __uint_as_float(__float_as_uint(r) + (__float_as_uint(t) << 31));
+}
+
+// acc + A*sin(rs) with the amplitude folded into the polynomial coefficients
+// (a = A, ac_i = A * kS_i): rs * (a + r2*(ac3 + r2*(ac5 + r2*(ac7 + r2*ac9)))) — 6 VALU ops
+// including the accumulate, so 11 per (sample, harmonic) with x = w*k and the reduction.
+__device__ __forceinline__ float amp_sin_acc(float rs, float a, float ac3, float ac5, float ac7,
+                                             float ac9, float acc) {
+  const float r2 = rs * rs;
+  float q = fmaf(ac9, r2, ac7);
+  q = fmaf(q, r2, ac5);
+  q = fmaf(q, r2, ac3);
+  q = fmaf(q, r2, a);
+  return fmaf(rs, q, acc);
+}
+
+// sin(x) for |x| < kFastArgLimit: abs error < 2e-7 (rms 4e-8 on uniform arguments).
+__device__ __forceinline__ float sin_reduced(float x) {
+  const float rs = reduce_signed(x);
+  const float r2 = rs * rs;
+  float q = fmaf(kS9, r2, kS7);
+  q = fmaf(q, r2, kS5);
+  q = fmaf(q, r2, kS3);
+  q = fmaf(q, r2, 1.0f);
+  return rs * q;
 }
 
 // Arguments beyond kFastArgLimit (long signals at high pitch): fp64 reduction of the

@@ -17,38 +17,67 @@
 #include <algorithm>
 
 #include "common.h"
+#include "twiddle4096.inc"
 
 namespace ddsp {
 namespace {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// cos(2*pi*q/n) table, q in [0, n): fp64-evaluated, rounded once.
+// cos(2*pi*q/n) table, q in [0, n): fp64-evaluated, rounded once — read from the FFT
+// twiddle table (same values) when n divides 4096, else computed in fp64.
 __device__ __forceinline__ void fill_cos_table(float* ct, int n) {
-  for (int q = threadIdx.x; q < n; q += blockDim.x) ct[q] = (float)cospi(2.0 * (double)q / (double)n);
+  if (4096 % n == 0) {
+    const int stride = 4096 / n;
+    for (int q = threadIdx.x; q < n; q += blockDim.x) ct[q] = kTwiddle4096[2 * q * stride];
+  } else {
+    for (int q = threadIdx.x; q < n; q += blockDim.x) ct[q] = (float)cospi(2.0 * (double)q / (double)n);
+  }
 }
 
 // irfft of NB real magnitudes (imaginary parts zero) at tap m: n = 2(NB-1),
 // (1/n)(A0 + (-1)^m A_{n/2} + 2 sum_{k=1}^{n/2-1} A_k cos(2 pi k m / n)).
+// The result is even in m (ir[n-m] == ir[m]), so callers evaluate m <= n/2 only.
 __device__ __forceinline__ float irfft_tap(const float* A, const float* ct, int n, int m) {
   const int half = n >> 1;
-  float acc = A[0] + ((m & 1) ? -A[half] : A[half]);
-  float acc2 = 0.0f;
-  int idx = m % n;  // (k*m) mod n, advanced incrementally
-  int km = idx;
-  for (int k = 1; k < half; ++k) {
-    acc2 = fmaf(A[k], ct[km], acc2);
-    km += idx;
-    if (km >= n) km -= n;
+  const float a0 = A[0] + ((m & 1) ? -A[half] : A[half]);
+  float s0 = 0.0f, s1 = 0.0f;
+  if ((n & (n - 1)) == 0) {  // power-of-two n: (k*m) mod n by mask, loads independent
+    const int mask = n - 1;
+    int k = 1;
+    for (; k + 1 < half; k += 2) {
+      s0 = fmaf(A[k], ct[(k * m) & mask], s0);
+      s1 = fmaf(A[k + 1], ct[((k + 1) * m) & mask], s1);
+    }
+    for (; k < half; ++k) s0 = fmaf(A[k], ct[(k * m) & mask], s0);
+  } else {
+    int km = m % n;
+    const int step = km;
+    for (int k = 1; k < half; ++k) {
+      s0 = fmaf(A[k], ct[km], s0);
+      km += step;
+      if (km >= n) km -= n;
+    }
   }
-  return (acc + 2.0f * acc2) / (float)n;
+  return (a0 + 2.0f * (s0 + s1)) / (float)n;
+}
+
+// ir[0..n) from its even half.
+__device__ __forceinline__ void irfft_taps(const float* A, const float* ct, int n, float* ir) {
+  const int half = n >> 1;
+  for (int m = threadIdx.x; m <= half; m += blockDim.x) {
+    const float v = irfft_tap(A, ct, n, m);
+    ir[m] = v;
+    if (m > 0 && m < half) ir[n - m] = v;
+  }
 }
 
 // Final filter value at position j of a target-length block (core.py:158-164):
 // imp1w[q] = ir[(q - n/2) mod n] * hann_n[q], padded/cropped to target, rolled by -n/2.
 __device__ __forceinline__ float ir_at(const float* ir, const float* ct, int n, int target, int j) {
   const int half = n >> 1;
-  const int q = (j + half) % target;
+  int q = j + half;  // (j + half) mod target, j < target
+  if (q >= target) q = half < target ? q - target : q % target;
   if (q >= n) return 0.0f;
   const float hann = 0.5f - 0.5f * ct[q];  // torch.hann_window(n), periodic
   int src = q - half;
@@ -95,7 +124,7 @@ __global__ void __launch_bounds__(256) impulse_response_kernel(const float* __re
   fill_cos_table(ct, n);
   for (int k = threadIdx.x; k < NB; k += blockDim.x) A[k] = amp[row * NB + k];
   __syncthreads();
-  for (int m = threadIdx.x; m < n; m += blockDim.x) ir[m] = irfft_tap(A, ct, n, m);
+  irfft_taps(A, ct, n, ir);
   __syncthreads();
   for (int j = threadIdx.x; j < target; j += blockDim.x)
     out[row * target + j] = ir_at(ir, ct, n, target, j);
@@ -154,7 +183,7 @@ __global__ void __launch_bounds__(256) filtered_noise_kernel(
     *reinterpret_cast<float4*>(x + 4 * t) = v;
   }
   __syncthreads();
-  for (int m = tid; m < n; m += NT) ir[m] = irfft_tap(A, ct, n, m);
+  irfft_taps(A, ct, n, ir);
   __syncthreads();
   for (int j = tid; j < bs4; j += NT) h[j] = j < bs ? ir_at(ir, ct, n, bs, j) : 0.0f;
   __syncthreads();

@@ -95,8 +95,9 @@ template <int SPT>
 __global__ void __launch_bounds__(256) harmonic_frames_kernel(
     const float* __restrict__ f0, const float* __restrict__ amp, float* dist, int write_back,
     float* __restrict__ out, int F, int H, int bs, float sr) {
-  extern __shared__ float4 smem4[];
-  float* amps = reinterpret_cast<float*>(smem4);  // H rounded up to 4, zero padded
+  // per harmonic k: coef[2k] = (A, A*S3, A*S5, A*S7), coef[2k+1] = (A*S9, k+1, A, 0), A = dist*amp;
+  // H rounded up to 4 with zero amplitudes.  Read back as wave-uniform (broadcast) LDS loads.
+  extern __shared__ float4 coef[];
   __shared__ double red[16];
 
   const int f = blockIdx.x;
@@ -120,7 +121,8 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
       v = dist[row * H + k] * a;
       if (write_back) dist[row * H + k] = v;
     }
-    amps[k] = v;
+    coef[2 * k] = make_float4(v, v * kS3, v * kS5, v * kS7);
+    coef[2 * k + 1] = make_float4(v * kS9, (float)(k + 1), v, 0.0f);
   }
   __syncthreads();
 
@@ -139,25 +141,22 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
       fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
     }
     if (fast) {
-      for (int k = 0; k < H4; k += 4) {
-        const float4 A = *reinterpret_cast<const float4*>(amps + k);
-        const float k0 = (float)(k + 1), k1 = (float)(k + 2), k2 = (float)(k + 3), k3 = (float)(k + 4);
+#pragma unroll 2
+      for (int k = 0; k < H4; ++k) {
+        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
 #pragma unroll
-        for (int s = 0; s < SPT; ++s) {
-          acc[s] = fmaf(sin_reduced(w[s] * k0), A.x, acc[s]);
-          acc[s] = fmaf(sin_reduced(w[s] * k1), A.y, acc[s]);
-          acc[s] = fmaf(sin_reduced(w[s] * k2), A.z, acc[s]);
-          acc[s] = fmaf(sin_reduced(w[s] * k3), A.w, acc[s]);
-        }
+        for (int s = 0; s < SPT; ++s)
+          acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
       }
     } else {
       for (int k = 0; k < H; ++k) {
-        const float kf = (float)(k + 1);
+        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
 #pragma unroll
         for (int s = 0; s < SPT; ++s) {
-          const float x = w[s] * kf;
-          const float sn = fabsf(x) < kFastArgLimit ? sin_reduced(x) : sin_slow(x);
-          acc[s] = fmaf(sn, amps[k], acc[s]);
+          const float x = w[s] * c1.y;
+          acc[s] = fabsf(x) < kFastArgLimit
+                       ? amp_sin_acc(reduce_signed(x), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
+                       : fmaf(sin_slow(x), c1.z, acc[s]);
         }
       }
     }
@@ -443,7 +442,7 @@ int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, flo
     return DDSP_HIP_EINVAL;
   int nt = (int)std::min<int64_t>(256, ((block_size / 2 + 63) / 64) * 64);
   nt = std::max(nt, 64);
-  const size_t shm = sizeof(float) * (size_t)((n_harmonic + 3) & ~3);
+  const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
   hipLaunchKernelGGL(harmonic_frames_kernel<2>, dim3((unsigned)frames, (unsigned)batch), dim3(nt),
                      shm, S(stream), f0, amplitudes, distribution, write_back, out, (int)frames,
                      (int)n_harmonic, (int)block_size, sample_rate);

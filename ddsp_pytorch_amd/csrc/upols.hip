@@ -77,41 +77,71 @@ __device__ __forceinline__ void dft16(float2 (&v)[16]) {
   for (int i = 0; i < 16; ++i) v[i] = t[i];
 }
 
-// One Stockham radix-16 pass on registers v (inputs in[j + 256 r]): twiddle, DFT16.
-// Output element r goes to index ((j/Ns)*Ns*16 + j%Ns) + r*Ns.
+// Twiddles w^r, r = 1..15, of one Stockham pass from four table loads (w, w^2, w^4, w^8):
+// every other power is a product of at most three table values (error <= ~3 ulp), so a pass
+// costs 4 global loads instead of 15 and they can be issued before the LDS phases.
+struct Tw4 {
+  float2 t1, t2, t4, t8;
+};
+
 template <bool INV>
-__device__ __forceinline__ void pass(float2 (&v)[16], int j, int Ns) {
-  const int k = j & (Ns - 1);
-  if (Ns > 1) {
-    const int step = k * (kN / (Ns * 16));
-#pragma unroll
-    for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], twiddle(r * step, INV));
-  }
-  dft16<INV>(v);
+__device__ __forceinline__ Tw4 load_tw(int step) {
+  Tw4 t;
+  t.t1 = twiddle(step, INV);
+  t.t2 = twiddle(2 * step, INV);
+  t.t4 = twiddle(4 * step, INV);
+  t.t8 = twiddle(8 * step, INV);
+  return t;
+}
+
+__device__ __forceinline__ void apply_tw(float2 (&v)[16], const Tw4& t) {
+  const float2 w3 = cmul(t.t1, t.t2), w5 = cmul(t.t4, t.t1), w6 = cmul(t.t4, t.t2);
+  const float2 w7 = cmul(t.t4, w3);
+  v[1] = cmul(v[1], t.t1);
+  v[2] = cmul(v[2], t.t2);
+  v[3] = cmul(v[3], w3);
+  v[4] = cmul(v[4], t.t4);
+  v[5] = cmul(v[5], w5);
+  v[6] = cmul(v[6], w6);
+  v[7] = cmul(v[7], w7);
+  v[8] = cmul(v[8], t.t8);
+  v[9] = cmul(v[9], cmul(t.t8, t.t1));
+  v[10] = cmul(v[10], cmul(t.t8, t.t2));
+  v[11] = cmul(v[11], cmul(t.t8, w3));
+  v[12] = cmul(v[12], cmul(t.t8, t.t4));
+  v[13] = cmul(v[13], cmul(t.t8, w5));
+  v[14] = cmul(v[14], cmul(t.t8, w6));
+  v[15] = cmul(v[15], cmul(t.t8, w7));
 }
 
 __device__ __forceinline__ int out_index(int j, int Ns, int r) {
   return (j / Ns) * Ns * 16 + (j & (Ns - 1)) + r * Ns;
 }
 
-// Full 4096-point transform: v holds in[j + 256 r] on entry and out[j + 256 r] on exit.
+// Full 4096-point transform (three radix-16 Stockham passes, Ns = 1, 16, 256):
+// v holds in[j + 256 r] on entry and out[j + 256 r] on exit.
 template <bool INV>
 __device__ __forceinline__ void fft4096(float2 (&v)[16], float2* lds) {
   const int j = threadIdx.x;
-  pass<INV>(v, j, 1);
+  // pass twiddle steps: k * N/(Ns*16) with k = j mod Ns
+  const Tw4 tw2 = load_tw<INV>((j & 15) * 16);
+  const Tw4 tw3 = load_tw<INV>(j);
+  dft16<INV>(v);
 #pragma unroll
   for (int r = 0; r < 16; ++r) lds[lds_idx(out_index(j, 1, r))] = v[r];
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = lds[lds_idx(j + 256 * r)];
   __syncthreads();
-  pass<INV>(v, j, 16);
+  apply_tw(v, tw2);
+  dft16<INV>(v);
 #pragma unroll
   for (int r = 0; r < 16; ++r) lds[lds_idx(out_index(j, 16, r))] = v[r];
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = lds[lds_idx(j + 256 * r)];
-  pass<INV>(v, j, 256);  // Ns = 256: output index == j + 256 r (coalesced)
+  apply_tw(v, tw3);
+  dft16<INV>(v);  // Ns = 256: output index == j + 256 r (coalesced)
 }
 
 // rows of the packed signal: pair -> (row_a, row_b or -1)
@@ -189,6 +219,7 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
     win[d] = (b0 + d < nb) ? Xp[(int64_t)(b0 + d) * kN] : make_float2(0.f, 0.f);
   }
   const int pmax = min(Q, b0 + kMacBlk);
+#pragma unroll 4
   for (int p = 0; p < pmax; ++p) {
     const float2 h = Hp[(int64_t)p * kN];
 #pragma unroll
