@@ -19,6 +19,7 @@
 #include "common.h"
 #include "twiddle4096.inc"
 
+
 namespace ddsp {
 namespace {
 
@@ -131,98 +132,151 @@ __global__ void __launch_bounds__(256) impulse_response_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------------
-// Fused FilteredNoise.forward: grid (frames, batch), block NT, 4 outputs per thread.
+// Fused FilteredNoise.forward: one wave (64 lanes) per frame, 4 frames per workgroup.
+// Per frame: magnitudes -> even half of the irfft taps (lane m: tap m; tap n/2 by a wave
+// reduction, since cos(pi k) = (-1)^k) -> rolled/windowed filter h[bs] in LDS -> noise
+// (Philox or injected) in LDS -> truncated causal convolution:
+//   * taps [0, n/2): 8 consecutive outputs per lane, a 12-float sliding window in registers,
+//     one float4 LDS read of noise and one of taps per 4 taps (32 FMAs);
+//   * taps (bs-n/2, bs) reach only the last n/2 outputs: lane l sums output bs-n/2+l
+//     directly into an LDS tail buffer, added when the outputs are written.
 // ---------------------------------------------------------------------------------
+constexpr int kNoiseFramesPerWG = 4;
+
 template <bool RNG>
 __global__ void __launch_bounds__(256) filtered_noise_kernel(
     const float* __restrict__ mags, const float* __restrict__ noise, uint32_t k0, uint32_t k1,
     uint32_t off0, uint32_t off1, const float* __restrict__ add, float* __restrict__ out,
-    float* __restrict__ noise_out, int F, int NB, int bs) {
+    float* __restrict__ noise_out, int64_t frames, int NB, int bs, int lo_end, int tail_start,
+    int pad, int per_frame) {
   extern __shared__ float4 smem4[];
   const int n = 2 * (NB - 1);
-  const int bs4 = (bs + 3) & ~3;
+  const int half = n >> 1;
   const int n4 = (n + 3) & ~3;
-  float* h = reinterpret_cast<float*>(smem4);  // [bs4]
-  float* xbuf = h + bs4;                        // [bs4 zeros | bs4 samples]
-  float* x = xbuf + bs4;
-  float* ct = x + bs4;                          // [n4]
-  float* ir = ct + n4;                          // [n4]
-  float* A = ir + n4;                           // [NB]
+  const int bs8 = (bs + 7) & ~7;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* ct = reinterpret_cast<float*>(smem4);       // [n4] shared cos table
+  float* base = ct + n4 + wv * per_frame;            // this wave's frame region
+  float* A = base;                                   // [NB -> 4]
+  float* ir = A + ((NB + 3) & ~3);                   // [n4]
+  float* h = ir + n4;                                // [bs8]
+  float* tail = h + bs8;                             // [half -> 4]
+  float* xbuf = tail + ((half + 3) & ~3);            // [pad zeros | bs8 samples]
+  float* x = xbuf + pad;
 
-  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, NT = blockDim.x;
-  const int64_t frame = (int64_t)b * F + f;
+  const int64_t frame = (int64_t)blockIdx.x * kNoiseFramesPerWG + wv;
+  const bool active = frame < frames;
 
   fill_cos_table(ct, n);
-  for (int k = tid; k < NB; k += NT) A[k] = mags[frame * NB + k];
-  for (int i = tid; i < bs4; i += NT) xbuf[i] = 0.0f;
-  const int quads = bs4 >> 2;
-  for (int t = tid; t < quads; t += NT) {
-    float4 v;
-    if (RNG) {
-      const uint64_t q = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
-      const Philox4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
-      v = make_float4(uniform_pm1(r.v[0]), uniform_pm1(r.v[1]), uniform_pm1(r.v[2]), uniform_pm1(r.v[3]));
-    } else {
-      const float* src = noise + frame * bs + 4 * t;
-      if ((bs & 3) == 0) {
-        v = *reinterpret_cast<const float4*>(src);
-      } else {
-        const int j = 4 * t;
-        v.x = j < bs ? src[0] : 0.f;
-        v.y = j + 1 < bs ? src[1] : 0.f;
-        v.z = j + 2 < bs ? src[2] : 0.f;
-        v.w = j + 3 < bs ? src[3] : 0.f;
-      }
-    }
-    if (RNG && (bs & 3)) {  // zero the lanes past the frame end
+  if (active) {
+    for (int k = lane; k < NB; k += 64) A[k] = mags[frame * NB + k];
+    for (int i = lane; i < pad; i += 64) xbuf[i] = 0.0f;
+    const int quads = bs8 >> 2;
+    const int fquads = ((bs + 3) & ~3) >> 2;  // counter stride per frame (as bs4/4)
+    for (int t = lane; t < quads; t += 64) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int j = 4 * t;
-      if (j + 1 >= bs) v.y = 0.f;
-      if (j + 2 >= bs) v.z = 0.f;
-      if (j + 3 >= bs) v.w = 0.f;
+      if (RNG) {
+        if (t < fquads) {
+          const uint64_t q = (uint64_t)frame * (uint64_t)fquads + (uint64_t)t;
+          const Philox4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
+          v = make_float4(uniform_pm1(r.v[0]), uniform_pm1(r.v[1]), uniform_pm1(r.v[2]),
+                          uniform_pm1(r.v[3]));
+        }
+        if (j >= bs) v.x = 0.f;
+        if (j + 1 >= bs) v.y = 0.f;
+        if (j + 2 >= bs) v.z = 0.f;
+        if (j + 3 >= bs) v.w = 0.f;
+      } else {
+        const float* src = noise + frame * bs;
+        if ((bs & 3) == 0) {
+          if (j < bs) v = *reinterpret_cast<const float4*>(src + j);
+        } else {
+          v.x = j < bs ? src[j] : 0.f;
+          v.y = j + 1 < bs ? src[j + 1] : 0.f;
+          v.z = j + 2 < bs ? src[j + 2] : 0.f;
+          v.w = j + 3 < bs ? src[j + 3] : 0.f;
+        }
+      }
+      *reinterpret_cast<float4*>(x + j) = v;
     }
-    *reinterpret_cast<float4*>(x + 4 * t) = v;
   }
   __syncthreads();
-  irfft_taps(A, ct, n, ir);
-  __syncthreads();
-  for (int j = tid; j < bs4; j += NT) h[j] = j < bs ? ir_at(ir, ct, n, bs, j) : 0.0f;
-  __syncthreads();
-
-  int lo_end = bs4, hi_start = bs4;
-  if (bs >= n) {
-    lo_end = std::min(((n >> 1) + 3) & ~3, bs4);
-    hi_start = std::max(((bs - (n >> 1)) & ~3), lo_end);
+  if (active) {
+    // even half of the taps; tap n/2 = (A0 + (-1)^{n/2} A_{n/2} + 2 sum_k (-1)^k A_k) / n
+    for (int m = lane; m < half; m += 64) ir[m] = irfft_tap(A, ct, n, m);
+    float alt = 0.0f;
+    for (int k = 1 + lane; k < half; k += 64) alt += (k & 1) ? -A[k] : A[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
+    if (lane == 0) ir[half] = (A[0] + ((half & 1) ? -A[half] : A[half]) + 2.0f * alt) / (float)n;
   }
+  __syncthreads();
+  if (active) {
+    for (int m = lane + 1; m < half; m += 64) ir[n - m] = ir[m];
+    for (int j = lane; j < bs8; j += 64) h[j] = j < bs ? ir_at(ir, ct, n, bs, j) : 0.0f;
+  }
+  __syncthreads();
+  if (active && tail_start < bs) {
+    // outputs j >= tail_start: sum_{m=tail_start}^{j} h[m] x[j-m]
+    for (int l = lane; l < bs - tail_start; l += 64) {
+      const int j = tail_start + l;
+      float c = 0.0f;
+      for (int d = 0; d <= l; ++d) c = fmaf(h[j - d], x[d], c);
+      tail[l] = c;
+    }
+  }
+  __syncthreads();
+  if (!active) return;
   float* ob = out + frame * bs;
-  for (int t = tid; t < quads; t += NT) {
-    const int j0 = 4 * t;
-    float4 y = fir4(h, x, j0, lo_end, hi_start, bs4);
-    if (noise_out) {
-      float* nb = noise_out + frame * bs;
-      if ((bs & 3) == 0) {
-        *reinterpret_cast<float4*>(nb + j0) = y;
-      } else {
-        const float yy[4] = {y.x, y.y, y.z, y.w};
-        for (int r = 0; r < 4; ++r) if (j0 + r < bs) nb[j0 + r] = yy[r];
-      }
+  const float* ab = add ? add + frame * bs : nullptr;
+  float* nb = noise_out ? noise_out + frame * bs : nullptr;
+  for (int j0 = 8 * lane; j0 < bs8; j0 += 512) {
+    float y[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) y[r] = 0.0f;
+    // window X[o + 4] = x[j0 - m + o], o in [-4, 8)
+    float X[12];
+    {
+      const float4 b0 = *reinterpret_cast<const float4*>(x + j0);
+      const float4 b1 = *reinterpret_cast<const float4*>(x + j0 + 4);
+      X[4] = b0.x; X[5] = b0.y; X[6] = b0.z; X[7] = b0.w;
+      X[8] = b1.x; X[9] = b1.y; X[10] = b1.z; X[11] = b1.w;
     }
-    if (add) {
-      const float* ab = add + frame * bs;
-      if ((bs & 3) == 0) {
-        const float4 a = *reinterpret_cast<const float4*>(ab + j0);
-        y.x += a.x; y.y += a.y; y.z += a.z; y.w += a.w;
-      } else {
-        y.x += ab[j0];
-        if (j0 + 1 < bs) y.y += ab[j0 + 1];
-        if (j0 + 2 < bs) y.z += ab[j0 + 2];
-        if (j0 + 3 < bs) y.w += ab[j0 + 3];
-      }
+    for (int m = 0; m < lo_end; m += 4) {
+      const float4 bm = *reinterpret_cast<const float4*>(x + j0 - m - 4);
+      X[0] = bm.x; X[1] = bm.y; X[2] = bm.z; X[3] = bm.w;
+      const float4 hh = *reinterpret_cast<const float4*>(h + m);
+      const float hd[4] = {hh.x, hh.y, hh.z, hh.w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) y[r] = fmaf(hd[d], X[r - d + 4], y[r]);
+#pragma unroll
+      for (int i = 11; i >= 4; --i) X[i] = X[i - 4];
     }
-    if ((bs & 3) == 0) {
-      *reinterpret_cast<float4*>(ob + j0) = y;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int j = j0 + r;
+      if (j >= tail_start && j < bs) y[r] += tail[j - tail_start];
+    }
+    if (nb) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (j0 + r < bs) nb[j0 + r] = y[r];
+    }
+    if (ab) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (j0 + r < bs) y[r] += ab[j0 + r];
+    }
+    if ((bs & 7) == 0) {
+      *reinterpret_cast<float4*>(ob + j0) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(ob + j0 + 4) = make_float4(y[4], y[5], y[6], y[7]);
     } else {
-      const float yy[4] = {y.x, y.y, y.z, y.w};
-      for (int r = 0; r < 4; ++r) if (j0 + r < bs) ob[j0 + r] = yy[r];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (j0 + r < bs) ob[j0 + r] = y[r];
     }
   }
 }
@@ -292,22 +346,40 @@ int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_
                             void* stream) {
   if (batch < 0 || frames < 0 || n_bands < 2 || block_size < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
-  if (!magnitudes || !out || batch > 65535 || frames > INT32_MAX) return DDSP_HIP_EINVAL;
-  const int64_t n = 2 * (n_bands - 1);
-  const int64_t bs4 = (block_size + 3) & ~3, n4 = (n + 3) & ~3, nb4 = (n_bands + 3) & ~3;
-  const size_t shm = sizeof(float) * (size_t)(3 * bs4 + 2 * n4 + nb4);
+  if (!magnitudes || !out || n_bands > 4097 || block_size > (1 << 16)) return DDSP_HIP_EINVAL;
+  const int n = 2 * (int)(n_bands - 1), half = n / 2, bs = (int)block_size;
+  const int n4 = (n + 3) & ~3, bs8 = (bs + 7) & ~7;
+  // taps [0, lo_end) by the windowed loop; (bs - n/2, bs) by the tail loop when the filter
+  // is shorter than the block (the usual case), else every tap by the windowed loop
+  int lo_end, tail_start;
+  if (bs >= n) {
+    lo_end = (half + 3) & ~3;
+    tail_start = bs - half;
+    if (tail_start < lo_end) {  // supports overlap: run every tap in the windowed loop
+      lo_end = bs8;
+      tail_start = bs;
+    }
+  } else {
+    lo_end = bs8;
+    tail_start = bs;
+  }
+  const int pad = ((lo_end + 4 + 7) & ~7);
+  const int per_frame = ((int)(n_bands + 3) & ~3) + n4 + bs8 + ((half + 3) & ~3) + pad + bs8;
+  const size_t shm = sizeof(float) * ((size_t)n4 + (size_t)kNoiseFramesPerWG * per_frame);
   if (shm > 160 * 1024) return DDSP_HIP_EINVAL;
-  const int nt = (int)std::min<int64_t>(256, std::max<int64_t>(64, ((bs4 / 4 + 63) / 64) * 64));
+  const int64_t total = batch * frames;
+  const int64_t blocks = (total + kNoiseFramesPerWG - 1) / kNoiseFramesPerWG;
+  if (blocks > INT32_MAX) return DDSP_HIP_EINVAL;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
   if (noise)
-    hipLaunchKernelGGL(filtered_noise_kernel<false>, dim3((unsigned)frames, (unsigned)batch), dim3(nt),
-                       shm, S(stream), magnitudes, noise, k0, k1, o0, o1, add, out, noise_out,
-                       (int)frames, (int)n_bands, (int)block_size);
+    hipLaunchKernelGGL(filtered_noise_kernel<false>, dim3((unsigned)blocks), dim3(256), shm, S(stream),
+                       magnitudes, noise, k0, k1, o0, o1, add, out, noise_out, total, (int)n_bands,
+                       bs, lo_end, tail_start, pad, per_frame);
   else
-    hipLaunchKernelGGL(filtered_noise_kernel<true>, dim3((unsigned)frames, (unsigned)batch), dim3(nt),
-                       shm, S(stream), magnitudes, nullptr, k0, k1, o0, o1, add, out, noise_out,
-                       (int)frames, (int)n_bands, (int)block_size);
+    hipLaunchKernelGGL(filtered_noise_kernel<true>, dim3((unsigned)blocks), dim3(256), shm, S(stream),
+                       magnitudes, nullptr, k0, k1, o0, o1, add, out, noise_out, total, (int)n_bands,
+                       bs, lo_end, tail_start, pad, per_frame);
   return launch_status();
 }
 
