@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--noise", choices=("device", "inject"), default="device")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-op-leg", action="store_true")
+    p.add_argument("--gather", action="store_true",
+                   help="N>1: also time synth + RCCL gather of the audio to rank 0 (reported "
+                        "separately as 'gathered'; value stays the sharded throughput)")
     p.add_argument("--cpu-batch", type=int, default=16, help="items in the CPU-baseline sample")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -213,6 +216,23 @@ def main():
         "roofline": roofline,
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
     }
+
+    if dist and args.gather:
+        from ddsp_pytorch_amd.shard import gather_audio
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        for _ in range(args.steps):
+            g = gather_audio(step(), B * world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter() - tg
+        tt = torch.tensor([tg], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        result["gathered"] = {"value": round(samples_per_step * args.steps / float(tt.item()), 1),
+                              "unit": "samples/s", "collective": "torch.distributed.gather (RCCL)",
+                              "ms_per_step": round(float(tt.item()) / args.steps * 1e3, 4)}
+        del g
 
     if rank == 0 and not args.no_op_leg:
         # op-boundary oscillator (core.py:136): per-sample inputs materialised in HBM
