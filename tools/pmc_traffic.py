@@ -29,7 +29,7 @@ REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch 
 
 
 def short(name):
-    base = name.split("(")[0]
+    base = name.replace("(anonymous namespace)", "anon").split("(")[0]
     base = base.replace("void ", "").split("::")[-1]
     return base.split("<")[0]
 
