@@ -154,8 +154,7 @@ def main():
                            args.sample_rate)
     inp = make_inputs(B, F, H, NB, bs, seed=rank, device=dev, with_noise=(args.noise == "inject"))
     syn = SynthPath(bs, sr, reverb_length=args.reverb_length, noise_mode=args.noise).to(dev)
-    timer = EventTimer(["harmonic_synth_frames", "filtered_noise", "reverb", "harmonic_controls",
-                        "noise_controls"])
+    timer = EventTimer(["harmonic_synth", "filtered_noise", "reverb"])
     syn.timer = timer
     core.set_noise_seed(1234 + rank)
 
@@ -190,19 +189,19 @@ def main():
     traffic = load_traffic(args.traffic)
 
     # dominant kernel: fused oscillator (per-launch = B*F*bs samples of this rank)
-    osc_ms = kern_ms["harmonic_synth_frames"]
+    osc_ms = kern_ms["harmonic_synth"]
     osc_bytes = 4 * (H + 2) * B * F * bs
     osc_gbs = osc_bytes / (osc_ms * 1e-3) / 1e9
     n_sin = B * F * bs * H
     roofline = {"bound": "hbm", "achieved": round(osc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(osc_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic.get("harmonic_frames_kernel"),
-                "kernel": "harmonic_frames_kernel<2> (fused HarmonicSynth.forward)",
+                "kernel": "harmonic_frames_kernel<2,true> (HarmonicSynth.get_controls+forward fused)",
                 "algorithmic_bytes_per_launch": osc_bytes, "avg_launch_ms": round(osc_ms, 4),
                 "convention": "SURVEY 8(d): 4*(H+2) B/sample op-boundary bytes credited to the fused "
                               "kernel; it physically reads only frame-rate controls",
                 "sines_per_s": round(n_sin / (osc_ms * 1e-3), 1),
-                "valu_bound_note": "fused kernel is VALU-bound: ~15 VALU ops per (sample, harmonic)"}
+                "valu_bound_note": "fused kernel is VALU-bound: 12 VALU ops per (sample, harmonic)"}
 
     result = {
         "metric": "audio samples/sec (48 kHz, 100 harm, blk=512) at 1/2/4/8 GPU; % HBM roofline",

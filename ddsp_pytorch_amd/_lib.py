@@ -36,7 +36,9 @@ SIGNATURES = {
     "ddsp_hip_fft_convolve": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_harmonic_controls": (_I, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _F, _P]),
     "ddsp_hip_harmonic_synth_frames": (_I, [_P, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _F, _P]),
+    "ddsp_hip_harmonic_synth_params": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_filtered_noise": (_I, [_P, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "ddsp_hip_filtered_noise_params": (_I, [_P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "ddsp_hip_reverb_build_impulse": (_I, [_P, _P, _P, _P, _I64, _F, _P]),
     "ddsp_hip_reverb_spectrum_floats": (_SZ, [_I64, _I64]),
     "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
-    "harmonic_synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
+    "harmonic_synth_frames", "harmonic_synth_params", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
     "reverb_spectrum", "reverb_apply", "set_noise_seed",
 ]
 
@@ -255,7 +255,24 @@ def set_noise_seed(seed):
     _noise_counter._offsets = itertools.count()
 
 
-def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=False):
+def harmonic_synth_params(f0, param, block_size, sample_rate):
+    """decoder.py:106-113 + modules.py:44-80 in one kernel: raw harmonic projection
+    param[B, F, H+1] (column 0 amplitude, 1..H distribution) and f0 [B, F, 1] -> audio
+    [B, F*block_size, 1].  The controls (scale, Nyquist mask, normalisation) never reach HBM."""
+    _dev(f0, param)
+    _no_grad_guard(f0, param)
+    B, F, H1 = param.shape
+    if f0.shape != (B, F, 1) or H1 < 2:
+        raise RuntimeError(f"harmonic_synth_params: f0 {tuple(f0.shape)} / param {tuple(param.shape)}")
+    f0c, pc = _c(f0), _c(param)
+    bs = int(block_size)
+    out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=f0.device)
+    _lib.call("harmonic_synth_params", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(out), B, F, H1 - 1, bs,
+              float(sample_rate), _lib.stream_of(out))
+    return out
+
+
+def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=False, raw_bias=None):
     """modules.py:116-128 FilteredNoise.forward, fused.
 
     magnitudes: [B, F, NB] (already scaled by get_controls).  ``noise`` [B, F, block_size]
@@ -282,8 +299,12 @@ def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=Fa
     out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=m.device)
     nout = torch.empty_like(out) if (return_noise and add is not None) else None
     seed, offset = _noise_counter.next() if noise is None else (0, 0)
-    _lib.call("filtered_noise", _lib.ptr(m), _lib.ptr(noise), seed, offset, _lib.ptr(add),
-              _lib.ptr(out), _lib.ptr(nout), B, F, NB, bs, _lib.stream_of(m))
+    if raw_bias is None:
+        _lib.call("filtered_noise", _lib.ptr(m), _lib.ptr(noise), seed, offset, _lib.ptr(add),
+                  _lib.ptr(out), _lib.ptr(nout), B, F, NB, bs, _lib.stream_of(m))
+    else:
+        _lib.call("filtered_noise_params", _lib.ptr(m), float(raw_bias), _lib.ptr(noise), seed, offset,
+                  _lib.ptr(add), _lib.ptr(out), _lib.ptr(nout), B, F, NB, bs, _lib.stream_of(m))
     if return_noise:
         return out, (nout if nout is not None else out)
     return out

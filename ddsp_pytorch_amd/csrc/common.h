@@ -78,6 +78,24 @@ __device__ __forceinline__ float sin_reduced(float x) {
   return rs * q;
 }
 
+constexpr float kLn10F = 2.30258512496948242188f;  // fl32(math.log(10)): ATen casts the exponent
+constexpr float kOnePlusEps = 1.0f + 1e-4f;          // (True).float() + 1e-4  in fp32
+constexpr float kEps = 0.0f + 1e-4f;                 // (False).float() + 1e-4 in fp32
+
+// ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7
+__device__ __forceinline__ float scale_fn(float x) {
+  float sig = 1.0f / (1.0f + expf(-x));
+  float p = powf(sig, kLn10F);
+  return 2.0f * p + 1e-7f;
+}
+
+// One harmonic-distribution entry of get_controls before normalisation (modules.py:53-60):
+// scale_function, then remove_above_nyquist's mask on fl32(f0 * (k+1)) (core.py:70-74).
+__device__ __forceinline__ float controls_value(float raw, float pitch0, int k, float half_sr) {
+  const float d = scale_fn(raw);
+  return d * ((pitch0 * (float)(k + 1)) < half_sr ? kOnePlusEps : kEps);
+}
+
 // Arguments beyond kFastArgLimit (long signals at high pitch): fp64 reduction of the
 // exact fp32 value and the fp64 sine, rounded.
 __device__ __noinline__ float sin_slow(float x) { return (float)sin((double)x); }

@@ -143,12 +143,14 @@ __global__ void __launch_bounds__(256) impulse_response_kernel(const float* __re
 // ---------------------------------------------------------------------------------
 constexpr int kNoiseFramesPerWG = 4;
 
-template <bool RNG>
+// RAW: `mags` are the raw noise projection (decoder.py:115), scaled here as
+// FilteredNoise.get_controls does (modules.py:111-114: scale_function(mags + bias)).
+template <bool RNG, bool RAW>
 __global__ void __launch_bounds__(256) filtered_noise_kernel(
     const float* __restrict__ mags, const float* __restrict__ noise, uint32_t k0, uint32_t k1,
     uint32_t off0, uint32_t off1, const float* __restrict__ add, float* __restrict__ out,
     float* __restrict__ noise_out, int64_t frames, int NB, int bs, int lo_end, int tail_start,
-    int pad, int per_frame) {
+    int pad, int per_frame, float bias) {
   extern __shared__ float4 smem4[];
   const int n = 2 * (NB - 1);
   const int half = n >> 1;
@@ -169,7 +171,10 @@ __global__ void __launch_bounds__(256) filtered_noise_kernel(
 
   fill_cos_table(ct, n);
   if (active) {
-    for (int k = lane; k < NB; k += 64) A[k] = mags[frame * NB + k];
+    for (int k = lane; k < NB; k += 64) {
+      const float m = mags[frame * NB + k];
+      A[k] = RAW ? scale_fn(m + bias) : m;
+    }
     for (int i = lane; i < pad; i += 64) xbuf[i] = 0.0f;
     const int quads = bs8 >> 2;
     const int fquads = ((bs + 3) & ~3) >> 2;  // counter stride per frame (as bs4/4)
@@ -340,10 +345,10 @@ int ddsp_hip_amp_to_impulse_response(const float* amp, float* impulse, int64_t r
   return launch_status();
 }
 
-int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_t seed,
-                            uint64_t offset, const float* add, float* out, float* noise_out,
-                            int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
-                            void* stream) {
+static int filtered_noise_launch(const float* magnitudes, bool raw, float bias, const float* noise,
+                                 uint64_t seed, uint64_t offset, const float* add, float* out,
+                                 float* noise_out, int64_t batch, int64_t frames, int64_t n_bands,
+                                 int64_t block_size, void* stream) {
   if (batch < 0 || frames < 0 || n_bands < 2 || block_size < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
   if (!magnitudes || !out || n_bands > 4097 || block_size > (1 << 16)) return DDSP_HIP_EINVAL;
@@ -372,15 +377,33 @@ int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_
   if (blocks > INT32_MAX) return DDSP_HIP_EINVAL;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
-  if (noise)
-    hipLaunchKernelGGL(filtered_noise_kernel<false>, dim3((unsigned)blocks), dim3(256), shm, S(stream),
-                       magnitudes, noise, k0, k1, o0, o1, add, out, noise_out, total, (int)n_bands,
-                       bs, lo_end, tail_start, pad, per_frame);
-  else
-    hipLaunchKernelGGL(filtered_noise_kernel<true>, dim3((unsigned)blocks), dim3(256), shm, S(stream),
-                       magnitudes, nullptr, k0, k1, o0, o1, add, out, noise_out, total, (int)n_bands,
-                       bs, lo_end, tail_start, pad, per_frame);
+#define DDSP_NOISE_LAUNCH(RNG_, RAW_)                                                          \
+  hipLaunchKernelGGL((filtered_noise_kernel<RNG_, RAW_>), dim3((unsigned)blocks), dim3(256), shm, \
+                     S(stream), magnitudes, noise, k0, k1, o0, o1, add, out, noise_out, total,  \
+                     (int)n_bands, bs, lo_end, tail_start, pad, per_frame, bias)
+  if (noise) {
+    if (raw) DDSP_NOISE_LAUNCH(false, true); else DDSP_NOISE_LAUNCH(false, false);
+  } else {
+    if (raw) DDSP_NOISE_LAUNCH(true, true); else DDSP_NOISE_LAUNCH(true, false);
+  }
+#undef DDSP_NOISE_LAUNCH
   return launch_status();
+}
+
+int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_t seed,
+                            uint64_t offset, const float* add, float* out, float* noise_out,
+                            int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
+                            void* stream) {
+  return filtered_noise_launch(magnitudes, false, 0.0f, noise, seed, offset, add, out, noise_out,
+                               batch, frames, n_bands, block_size, stream);
+}
+
+int ddsp_hip_filtered_noise_params(const float* raw_magnitudes, float bias, const float* noise,
+                                   uint64_t seed, uint64_t offset, const float* add, float* out,
+                                   float* noise_out, int64_t batch, int64_t frames, int64_t n_bands,
+                                   int64_t block_size, void* stream) {
+  return filtered_noise_launch(raw_magnitudes, true, bias, noise, seed, offset, add, out, noise_out,
+                               batch, frames, n_bands, block_size, stream);
 }
 
 }  // extern "C"

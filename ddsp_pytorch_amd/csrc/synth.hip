@@ -17,16 +17,6 @@
 namespace ddsp {
 namespace {
 
-constexpr float kLn10F = 2.30258512496948242188f;  // fl32(math.log(10)): ATen casts the exponent
-constexpr float kOnePlusEps = 1.0f + 1e-4f;          // (True).float() + 1e-4  in fp32
-constexpr float kEps = 0.0f + 1e-4f;                 // (False).float() + 1e-4 in fp32
-
-__device__ __forceinline__ float scale_fn(float x) {
-  // ddsp/core.py:77-78  2 * sigmoid(x) ** ln(10) + 1e-7
-  float sig = 1.0f / (1.0f + expf(-x));
-  float p = powf(sig, kLn10F);
-  return 2.0f * p + 1e-7f;
-}
 
 __global__ void scale_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                              float bias) {
@@ -62,7 +52,9 @@ __global__ void upsample_kernel(const float* __restrict__ x, float* __restrict__
   }
 }
 
-// HarmonicSynth.get_controls (modules.py:44-67): one wave per frame row.
+// HarmonicSynth.get_controls (modules.py:44-67): one wave per frame row, the row's values
+// held in registers (H <= 64*kCtlPer) between the sum and the normalisation.
+constexpr int kCtlPer = 4;
 __global__ void __launch_bounds__(256) harmonic_controls_kernel(
     const float* __restrict__ amp_raw, int64_t amp_stride, const float* __restrict__ dist_raw,
     int64_t dist_stride, const float* __restrict__ f0, float* __restrict__ amplitudes,
@@ -73,17 +65,28 @@ __global__ void __launch_bounds__(256) harmonic_controls_kernel(
   const float pitch0 = f0[r];
   const float* drow = dist_raw + r * dist_stride;
   float* orow = dist + r * (int64_t)H;
+  float d[kCtlPer];
   double sum = 0.0;
-  for (int k = lane; k < H; k += 64) {
-    float d = scale_fn(drow[k]);
-    d = d * ((pitch0 * (float)(k + 1)) < half_sr ? kOnePlusEps : kEps);
-    orow[k] = d;
-    sum += (double)d;
+#pragma unroll
+  for (int i = 0; i < kCtlPer; ++i) {
+    const int k = lane + 64 * i;
+    d[i] = k < H ? controls_value(drow[k], pitch0, k, half_sr) : 0.0f;
+    sum += (double)d[i];
+  }
+  for (int k = lane + 64 * kCtlPer; k < H; k += 64) {  // H > 256: spill to the output row
+    const float v = controls_value(drow[k], pitch0, k, half_sr);
+    orow[k] = v;
+    sum += (double)v;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
   const float s = (float)sum;
-  for (int k = lane; k < H; k += 64) orow[k] = orow[k] / s;  // dist /= dist.sum(-1)
+#pragma unroll
+  for (int i = 0; i < kCtlPer; ++i) {
+    const int k = lane + 64 * i;
+    if (k < H) orow[k] = d[i] / s;  // dist /= dist.sum(-1)
+  }
+  for (int k = lane + 64 * kCtlPer; k < H; k += 64) orow[k] = orow[k] / s;
   if (lane == 0) amplitudes[r] = scale_fn(amp_raw[r * amp_stride]);
 }
 
@@ -91,7 +94,10 @@ __global__ void __launch_bounds__(256) harmonic_controls_kernel(
 // Fused HarmonicSynth.forward (modules.py:69-80) at frame rate.
 // grid (frames, batch); block NT threads; each thread SPT samples of the frame per pass.
 // ---------------------------------------------------------------------------------
-template <int SPT>
+// RAW = true: `dist` is the raw parameter row [B,F,H+1] (decoder.py:106-108 split), and the
+// controls of modules.py:44-67 (scale, Nyquist mask, normalise, times the scaled amplitude) are
+// computed in the prologue — HarmonicSynth.get_controls + forward in one launch.
+template <int SPT, bool RAW>
 __global__ void __launch_bounds__(256) harmonic_frames_kernel(
     const float* __restrict__ f0, const float* __restrict__ amp, float* dist, int write_back,
     float* __restrict__ out, int F, int H, int bs, float sr) {
@@ -113,13 +119,32 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
 
   // stage this frame's harmonic amplitudes dist[k] * amp (modules.py:73, in place if asked)
   const int64_t row = (int64_t)b * F + f;
-  const float a = amp[row];
   const int H4 = (H + 3) & ~3;
+  float a, norm = 1.0f;
+  if (RAW) {
+    const float* prow = dist + row * (H + 1);
+    const float half_sr = sr * 0.5f;
+    const float pitch0 = f0b[f];
+    double part2 = 0.0;
+    for (int k = tid; k < H; k += NT) {
+      const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+      coef[2 * k].x = v;
+      part2 += (double)v;
+    }
+    norm = (float)block_sum_double(part2, red);  // dist.sum(-1)
+    a = scale_fn(prow[0]);
+  } else {
+    a = amp[row];
+  }
   for (int k = tid; k < H4; k += NT) {
     float v = 0.0f;
     if (k < H) {
-      v = dist[row * H + k] * a;
-      if (write_back) dist[row * H + k] = v;
+      if (RAW) {
+        v = (coef[2 * k].x / norm) * a;  // (dist / sum) * amp, the reference's rounding order
+      } else {
+        v = dist[row * H + k] * a;
+        if (write_back) dist[row * H + k] = v;
+      }
     }
     coef[2 * k] = make_float4(v, v * kS3, v * kS5, v * kS7);
     coef[2 * k + 1] = make_float4(v * kS9, (float)(k + 1), v, 0.0f);
@@ -443,8 +468,25 @@ int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, flo
   int nt = (int)std::min<int64_t>(256, ((block_size / 2 + 63) / 64) * 64);
   nt = std::max(nt, 64);
   const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
-  hipLaunchKernelGGL(harmonic_frames_kernel<2>, dim3((unsigned)frames, (unsigned)batch), dim3(nt),
+  hipLaunchKernelGGL((harmonic_frames_kernel<2, false>), dim3((unsigned)frames, (unsigned)batch), dim3(nt),
                      shm, S(stream), f0, amplitudes, distribution, write_back, out, (int)frames,
+                     (int)n_harmonic, (int)block_size, sample_rate);
+  return launch_status();
+}
+
+int ddsp_hip_harmonic_synth_params(const float* f0, const float* param, float* out, int64_t batch,
+                                   int64_t frames, int64_t n_harmonic, int64_t block_size,
+                                   float sample_rate, void* stream) {
+  if (batch < 0 || frames < 0 || n_harmonic < 1 || block_size < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
+  if (!f0 || !param || !out) return DDSP_HIP_EINVAL;
+  if (frames > INT32_MAX || batch > 65535 || n_harmonic > 8192 || block_size > (1 << 20))
+    return DDSP_HIP_EINVAL;
+  int nt = (int)std::min<int64_t>(256, ((block_size / 2 + 63) / 64) * 64);
+  nt = std::max(nt, 64);
+  const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
+  hipLaunchKernelGGL((harmonic_frames_kernel<2, true>), dim3((unsigned)frames, (unsigned)batch), dim3(nt),
+                     shm, S(stream), f0, nullptr, const_cast<float*>(param), 0, out, (int)frames,
                      (int)n_harmonic, (int)block_size, sample_rate);
   return launch_status();
 }

@@ -3,8 +3,8 @@ frame-rate controls -> harmonic + filtered noise -> reverb -> audio.
 
 This is the unit the benchmark times (SURVEY.md §8(d) "End-to-end unit"): raw
 harmonic parameters [B,F,H+1], pitch [B,F,1] and raw noise magnitudes [B,F,NB] in,
-audio [B,F*bs,1] out.  Kernels per call: harmonic controls, fused oscillator bank,
-noise-magnitude scaling, fused filtered noise (+ harmonic sum), reverb (rocFFT).
+audio [B,F*bs,1] out.  Kernels per call: oscillator bank fused with its controls,
+fused filtered noise with its controls (+ harmonic sum), reverb (partitioned FFT).
 """
 import torch
 import torch.nn as nn
@@ -54,20 +54,20 @@ class SynthPath(nn.Module):
 
     @torch.no_grad()
     def forward(self, f0, param, mags, noise=None):
-        with self._t("harmonic_controls"):
-            amps, dist = core.harmonic_controls(param[..., :1], param[..., 1:], f0, self.sample_rate)
-        with self._t("harmonic_synth_frames"):
-            harmonic = core.harmonic_synth_frames(f0, amps, dist, self.block_size, self.sample_rate,
-                                                  write_back=False)
-        with self._t("noise_controls"):
-            m = core.scale_with_bias(mags, self.initial_bias)
+        # HarmonicSynth.get_controls + forward (modules.py:44-80) in one kernel
+        with self._t("harmonic_synth"):
+            harmonic = core.harmonic_synth_params(f0, param, self.block_size, self.sample_rate)
+        # FilteredNoise.get_controls + forward (modules.py:111-128) + `harmonic + noise`
+        # (decoder.py:121) in one kernel
         with self._t("filtered_noise"):
             if self.noise_mode == "inject":
                 if noise is None:
                     raise ValueError("noise_mode='inject' needs a noise tensor")
-                signal = core.filtered_noise(m, self.block_size, noise=noise, add=harmonic)
+                signal = core.filtered_noise(mags, self.block_size, noise=noise, add=harmonic,
+                                             raw_bias=self.initial_bias)
             else:
-                signal = core.filtered_noise(m, self.block_size, add=harmonic)
+                signal = core.filtered_noise(mags, self.block_size, add=harmonic,
+                                             raw_bias=self.initial_bias)
         if self.reverb is not None:
             with self._t("reverb"):
                 signal = self.reverb(signal)

@@ -100,6 +100,13 @@ int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, flo
                                    int64_t n_harmonic, int64_t block_size, float sample_rate,
                                    void* stream);
 
+/* decoder.py:106-113 + modules.py:44-80: HarmonicSynth.get_controls and forward in one launch,
+ * straight from the harmonic projection param[B,F,H+1] (amplitude column 0, distribution
+ * columns 1..H, decoder.py:107-108).  The controls never reach HBM. */
+int ddsp_hip_harmonic_synth_params(const float* f0, const float* param, float* out, int64_t batch,
+                                   int64_t frames, int64_t n_harmonic, int64_t block_size,
+                                   float sample_rate, void* stream);
+
 /* modules.py:116-128  FilteredNoise.forward fused: per-frame zero-phase FIR from the
  * magnitudes (amp_to_impulse_response) applied to block_size noise samples by truncated
  * linear convolution (fft_convolve).  noise == NULL draws U[-1,1) on device
@@ -111,6 +118,15 @@ int ddsp_hip_filtered_noise(const float* magnitudes, const float* noise, uint64_
                             uint64_t offset, const float* add, float* out, float* noise_out,
                             int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
                             void* stream);
+
+/* modules.py:111-128  FilteredNoise.get_controls + forward in one launch: raw_magnitudes is the
+ * noise projection [B,F,NB] (decoder.py:115); the kernel applies scale_function(x + bias)
+ * (bias = initial_bias, -5 by default) before designing the filters.  Other arguments as
+ * ddsp_hip_filtered_noise. */
+int ddsp_hip_filtered_noise_params(const float* raw_magnitudes, float bias, const float* noise,
+                                   uint64_t seed, uint64_t offset, const float* add, float* out,
+                                   float* noise_out, int64_t batch, int64_t frames, int64_t n_bands,
+                                   int64_t block_size, void* stream);
 
 /* modules.py:21-26  Reverb.build_impulse: noise[L]*exp(-softplus(-decay)*t*500)*sigmoid(wet),
  * impulse[0] = 1.  decay and wet are device scalars. */

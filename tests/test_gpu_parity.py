@@ -275,3 +275,36 @@ def test_config2_synth_path(dd):
                             inp["noise"][sl].cpu(), rv, 512, 48000)
         e = rms(C(out[sl]), ref.numpy())
         assert e < PARITY_RMS, (b, e)
+
+
+# ------------------------------------------------------------------ fused-controls kernels
+@pytest.mark.parametrize("name", ["g2_controls", "g2_controls_rt"])
+def test_harmonic_params_golden(dd, name):
+    """get_controls + forward in one kernel, straight from the raw projection."""
+    g = load_golden(name)
+    with torch.no_grad():
+        out = C(dd.core.harmonic_synth_params(G(g["f0"]), G(g["param"]), int(g["block_size"]), 48000))
+    assert rms(out, g["out"]) < 1e-6, rms(out, g["out"])
+
+
+def test_noise_params_golden(dd):
+    g = load_golden("g3_noise")
+    with torch.no_grad():
+        out = C(dd.core.filtered_noise(G(g["mags"]), 512, noise=G(g["noise_in"]), raw_bias=-5.0))
+    assert rms(out, g["out"]) < 1e-7, rms(out, g["out"])
+
+
+@pytest.mark.parametrize("nb_blocks,L", [(3, 300), (50, 48000), (100, 48000), (50, 96000), (120, 250000)])
+def test_reverb_partitioned_shapes(dd, nb_blocks, L):
+    """UPOLS (LDS-tiled MAC and the global-memory MAC for very long IRs) vs fp64 convolution."""
+    T = nb_blocks * 2048 - 17
+    rng = np.random.default_rng(L + T)
+    x = (rng.standard_normal((3, T, 1)) * 0.3).astype(np.float32)
+    h = (rng.standard_normal(L) * np.exp(-np.arange(L) / 8000.0)).astype(np.float32)
+    h[0] = 1.0
+    with torch.no_grad():
+        spec = dd.core.reverb_spectrum(G(h), T)
+        out = C(dd.core.reverb_apply(G(x), spec, L))
+    ref = no.reverb(x, h)
+    scale = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    assert rms(out, ref) < 1e-6 * scale, (rms(out, ref), scale)

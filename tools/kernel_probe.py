@@ -1,0 +1,43 @@
+"""Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
+
+    python tools/kernel_probe.py {harmonic,harmonic_frames,noise,reverb,op} [reps]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ddsp_pytorch_amd import core  # noqa: E402
+from ddsp_pytorch_amd.synth import SynthPath, make_inputs  # noqa: E402
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "harmonic"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    dev = torch.device("cuda", 0)
+    B, F, H, NB, bs, sr = 64, 200, 100, 65, 512, 48000
+    inp = make_inputs(B, F, H, NB, bs, seed=0, device=dev, with_noise=False)
+    syn = SynthPath(bs, sr, reverb_length=48000).to(dev)
+    with torch.no_grad():
+        amps, dist = core.harmonic_controls(inp["param"][..., :1], inp["param"][..., 1:], inp["f0"], sr)
+        x = torch.randn(B, F * bs, 1, device=dev)
+        if which == "op":
+            f0s = core.upsample(inp["f0"], bs)
+            a = core.upsample(dist, bs)
+        for _ in range(reps):
+            if which == "harmonic":
+                core.harmonic_synth_params(inp["f0"], inp["param"], bs, sr)
+            elif which == "harmonic_frames":
+                core.harmonic_synth_frames(inp["f0"], amps, dist, bs, sr, write_back=False)
+            elif which == "noise":
+                core.filtered_noise(inp["mags"], bs, add=x, raw_bias=-5.0)
+            elif which == "reverb":
+                syn.reverb(x)
+            elif which == "op":
+                core.harmonic_synth(f0s, a, sr)
+        torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
