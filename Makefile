@@ -11,7 +11,12 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 HIPFLAGS_synth := -fno-slp-vectorize
 OBJ := $(patsubst ddsp_pytorch_amd/csrc/%.hip,build/%.o,$(SRC))
 
-all: $(LIB)
+TORCH_DIR := $(shell python3 -c "import torch,os;print(os.path.dirname(torch.__file__))" 2>/dev/null)
+TORCH_LIB := ddsp_pytorch_amd/lib/libddsp_hip_torch.so
+
+RT_HOST := tools/realtime_host
+
+all: $(LIB) $(TORCH_LIB) $(RT_HOST)
 
 build/twiddle4096.inc: tools/gen_twiddles.py
 	@mkdir -p build
@@ -27,7 +32,20 @@ $(LIB): $(OBJ)
 	@mkdir -p ddsp_pytorch_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
 
+# TorchScript operators torch.ops.ddsp_hip.* (host C++ over the C-ABI; no device code)
+$(TORCH_LIB): ddsp_pytorch_amd/csrc/torch_ops.cpp include/ddsp_hip.h $(LIB)
+	g++ -O2 -std=c++17 -shared -fPIC -o $@ $< -Iinclude -I$(TORCH_DIR)/include \
+	  -I$(TORCH_DIR)/include/torch/csrc/api/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__=1 \
+	  -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI=1 -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu \
+	  -ltorch_hip -Lddsp_pytorch_amd/lib -lddsp_hip -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
+
+# C++ libtorch realtime host mirroring the ddsp~ external (config 3 latency)
+$(RT_HOST): tools/realtime_host.cpp
+	g++ -O2 -std=c++17 $< -o $@ -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include \
+	  -D_GLIBCXX_USE_CXX11_ABI=1 -L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -lc10 -Wl,--no-as-needed \
+	  -ltorch_hip -Wl,--as-needed -Wl,-rpath,$(TORCH_DIR)/lib -ldl -lpthread
+
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TORCH_LIB) $(RT_HOST)
 
 .PHONY: all clean

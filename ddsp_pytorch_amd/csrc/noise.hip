@@ -209,7 +209,21 @@ __global__ void __launch_bounds__(256) filtered_noise_kernel(
   __syncthreads();
   if (active) {
     // even half of the taps; tap n/2 = (A0 + (-1)^{n/2} A_{n/2} + 2 sum_k (-1)^k A_k) / n
-    for (int m = lane; m < half; m += 64) ir[m] = irfft_tap(A, ct, n, m);
+    if (n == 128) {
+      // 65 bands -> 128 taps (the reference's default window_size): read the irfft matrix
+      // from a code-object table, coalesced across lanes (no LDS gather, no bank conflicts)
+      const int m = lane;
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 8
+      for (int k = 1; k < 63; k += 2) {
+        s0 = fmaf(A[k], kIrCos128[k * 64 + m], s0);
+        s1 = fmaf(A[k + 1], kIrCos128[(k + 1) * 64 + m], s1);
+      }
+      s0 = fmaf(A[63], kIrCos128[63 * 64 + m], s0);
+      ir[m] = (A[0] + ((m & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
+    } else {
+      for (int m = lane; m < half; m += 64) ir[m] = irfft_tap(A, ct, n, m);
+    }
     float alt = 0.0f;
     for (int k = 1 + lane; k < half; k += 64) alt += (k & 1) ? -A[k] : A[k];
 #pragma unroll
