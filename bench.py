@@ -41,24 +41,35 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch", type=int, default=64, help="items per GPU")
-    p.add_argument("--frames", type=int, default=200)
+    p.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                   help="BASELINE.json configuration: 2 (default; batch 64, 200 frames, 100 "
+                        "harmonics, 1 s IR), 4 (batch 16, 2 s IR), 5 (per-GPU shard of the 8-GPU "
+                        "job: batch 64, 400 frames, 128 harmonics)")
+    p.add_argument("--batch", type=int, default=None, help="items per GPU")
+    p.add_argument("--frames", type=int, default=None)
     p.add_argument("--block-size", type=int, default=512)
-    p.add_argument("--harmonics", type=int, default=100)
+    p.add_argument("--harmonics", type=int, default=None)
     p.add_argument("--bands", type=int, default=65)
     p.add_argument("--sample-rate", type=int, default=48000)
-    p.add_argument("--reverb-length", type=int, default=48000)
+    p.add_argument("--reverb-length", type=int, default=None)
     p.add_argument("--noise", choices=("device", "inject"), default="device")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-op-leg", action="store_true")
     p.add_argument("--gather", action="store_true",
                    help="N>1: also time synth + RCCL gather of the audio to rank 0 (reported "
                         "separately as 'gathered'; value stays the sharded throughput)")
-    p.add_argument("--cpu-batch", type=int, default=16, help="items in the CPU-baseline sample")
+    p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC HBM bytes per launch (tools/pmc_traffic.py output)")
-    return p.parse_args()
+    a = p.parse_args()
+    cfg = {2: (64, 200, 100, 48000), 4: (16, 200, 100, 96000), 5: (64, 400, 128, 48000)}[a.config]
+    if a.cpu_batch is None:
+        a.cpu_batch = 8 if a.config == 5 else 16
+    for name, v in zip(("batch", "frames", "harmonics", "reverb_length"), cfg):
+        if getattr(a, name) is None:
+            setattr(a, name, v)
+    return a
 
 
 class EventTimer:
@@ -128,8 +139,9 @@ def cpu_baseline(args, rank_inputs_seed=0):
     samples = B * args.frames * args.block_size
     return {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"oracle/torch_ref.synth_path (reference ATen op sequence), batch {B} of "
-                      f"config 2 (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
-                      f"NB={args.bands}, 1 s reverb), median of {len(times)} runs, {t:.3f} s each"}
+                      f"config {args.config} (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
+                      f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {len(times)} runs, "
+                      f"{t:.3f} s each"}
 
 
 def main():
@@ -209,7 +221,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": f"synthetic (SURVEY 8(d) seeded controls; noise {'on-device Philox' if args.noise == 'device' else 'injected'})",
-        "config": {"workload": f"config 2 synth path: batch {B}/GPU, frames {F}, block_size {bs}, "
+        "config": {"workload": f"config {args.config} synth path: batch {B}/GPU, frames {F}, block_size {bs}, "
                                f"n_harmonic {H}, n_bands {NB}, sr {sr}, reverb {args.reverb_length} taps",
                    "global_batch": B * world, "seq_len": F * bs, "parallelism": f"batch-shard x{world}"},
         "roofline": roofline,

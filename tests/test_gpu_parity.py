@@ -308,3 +308,33 @@ def test_reverb_partitioned_shapes(dd, nb_blocks, L):
     ref = no.reverb(x, h)
     scale = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
     assert rms(out, ref) < 1e-6 * scale, (rms(out, ref), scale)
+
+
+# ------------------------------------------------------------------ configs 4 and 5
+def test_config4_long_ir_reverb(dd):
+    """Config 4: 2 s impulse response (Reverb(96000, 48000)) on 102400-sample items."""
+    rv = dd.Reverb(96000, 48000).cuda()
+    x = torch.randn(4, 102400, 1, device="cuda") * 0.3
+    with torch.no_grad():
+        out = C(rv(x))
+        imp = C(rv.build_impulse())
+    ref = no.reverb(C(x), imp)
+    scale = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    assert rms(out, ref) < 1e-6 * scale
+
+
+def test_config5_synth_path_items(dd):
+    """Config 5 shard shape: 400 frames, 128 harmonics (|arg| up to ~3.4e6 rad); two items of a
+    64-item shard against the torch-CPU restatement of the reference."""
+    from ddsp_pytorch_amd.synth import make_inputs, SynthPath
+    inp = make_inputs(64, 400, 128, 65, 512, seed=5, device="cuda")
+    syn = SynthPath(512, 48000, reverb_length=48000, noise_mode="inject").cuda()
+    with torch.no_grad():
+        out = syn(inp["f0"], inp["param"], inp["mags"], inp["noise"])
+    rv = tr.Reverb(syn.reverb.noise.detach().cpu(), syn.reverb.decay.detach().cpu(),
+                   syn.reverb.wet.detach().cpu(), 48000, 48000)
+    for b in (3, 60):
+        sl = slice(b, b + 1)
+        ref = tr.synth_path(inp["f0"][sl].cpu(), inp["param"][sl].cpu(), inp["mags"][sl].cpu(),
+                            inp["noise"][sl].cpu(), rv, 512, 48000)
+        assert rms(C(out[sl]), ref.numpy()) < PARITY_RMS
