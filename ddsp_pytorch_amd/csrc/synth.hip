@@ -405,6 +405,24 @@ inline unsigned grid1d(int64_t n, int nt) {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// One workgroup per (frame, item).  4 samples per thread when the block is long enough
+// (more independent sine chains per lane: measured 4% faster than 2 at block 512), else 2.
+template <bool RAW>
+void launch_frames(const float* f0, const float* amp, float* dist, int write_back, float* out,
+                   int64_t batch, int64_t frames, int64_t H, int64_t bs, float sr, size_t shm,
+                   void* stream) {
+  const dim3 grid((unsigned)frames, (unsigned)batch);
+  if (bs >= 256) {
+    const int nt = (int)std::min<int64_t>(256, ((bs / 4 + 63) / 64) * 64);
+    hipLaunchKernelGGL((harmonic_frames_kernel<4, RAW>), grid, dim3(nt), shm, S(stream), f0, amp, dist,
+                       write_back, out, (int)frames, (int)H, (int)bs, sr);
+  } else {
+    const int nt = (int)std::max<int64_t>(64, ((bs / 2 + 63) / 64) * 64);
+    hipLaunchKernelGGL((harmonic_frames_kernel<2, RAW>), grid, dim3(nt), shm, S(stream), f0, amp, dist,
+                       write_back, out, (int)frames, (int)H, (int)bs, sr);
+  }
+}
+
 }  // namespace
 }  // namespace ddsp
 
@@ -465,12 +483,9 @@ int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, flo
   if (!f0 || !amplitudes || !distribution || !out) return DDSP_HIP_EINVAL;
   if (frames > INT32_MAX || batch > 65535 || n_harmonic > 8192 || block_size > (1 << 20))
     return DDSP_HIP_EINVAL;
-  int nt = (int)std::min<int64_t>(256, ((block_size / 2 + 63) / 64) * 64);
-  nt = std::max(nt, 64);
   const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
-  hipLaunchKernelGGL((harmonic_frames_kernel<2, false>), dim3((unsigned)frames, (unsigned)batch), dim3(nt),
-                     shm, S(stream), f0, amplitudes, distribution, write_back, out, (int)frames,
-                     (int)n_harmonic, (int)block_size, sample_rate);
+  launch_frames<false>(f0, amplitudes, distribution, write_back, out, batch, frames, n_harmonic,
+                       block_size, sample_rate, shm, stream);
   return launch_status();
 }
 
@@ -482,12 +497,9 @@ int ddsp_hip_harmonic_synth_params(const float* f0, const float* param, float* o
   if (!f0 || !param || !out) return DDSP_HIP_EINVAL;
   if (frames > INT32_MAX || batch > 65535 || n_harmonic > 8192 || block_size > (1 << 20))
     return DDSP_HIP_EINVAL;
-  int nt = (int)std::min<int64_t>(256, ((block_size / 2 + 63) / 64) * 64);
-  nt = std::max(nt, 64);
   const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
-  hipLaunchKernelGGL((harmonic_frames_kernel<2, true>), dim3((unsigned)frames, (unsigned)batch), dim3(nt),
-                     shm, S(stream), f0, nullptr, const_cast<float*>(param), 0, out, (int)frames,
-                     (int)n_harmonic, (int)block_size, sample_rate);
+  launch_frames<true>(f0, nullptr, const_cast<float*>(param), 0, out, batch, frames, n_harmonic,
+                      block_size, sample_rate, shm, stream);
   return launch_status();
 }
 
