@@ -82,10 +82,12 @@ constexpr float kLn10F = 2.30258512496948242188f;  // fl32(math.log(10)): ATen c
 constexpr float kOnePlusEps = 1.0f + 1e-4f;          // (True).float() + 1e-4  in fp32
 constexpr float kEps = 0.0f + 1e-4f;                 // (False).float() + 1e-4 in fp32
 
-// ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7
+// ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7.  sigmoid(x)**ln10 as
+// exp2(ln10 * log2(sigmoid)) on the hardware log/exp (relative error <~1e-6 for sigmoid >= 1e-3,
+// vs ~1 ulp for powf): 4% of the fused oscillator's time for a 1e-7-level amplitude change.
 __device__ __forceinline__ float scale_fn(float x) {
-  float sig = 1.0f / (1.0f + expf(-x));
-  float p = powf(sig, kLn10F);
+  const float sig = 1.0f / (1.0f + expf(-x));
+  const float p = exp2f(kLn10F * log2f(sig));
   return 2.0f * p + 1e-7f;
 }
 
