@@ -168,7 +168,7 @@ def main():
     syn = SynthPath(bs, sr, reverb_length=args.reverb_length, noise_mode=args.noise).to(dev)
     # timed region: events only around the dominant kernel (the roofline's launch duration);
     # the per-kernel breakdown is measured in a separate loop afterwards
-    timer = EventTimer(["harmonic_synth"])
+    timer = EventTimer(["synth_frames"])
     syn.timer = timer
     core.set_noise_seed(1234 + rank)
 
@@ -197,7 +197,7 @@ def main():
         elapsed = float(t.item())
     assert torch.isfinite(out).all()
 
-    breakdown = EventTimer(["harmonic_synth", "filtered_noise", "reverb"])
+    breakdown = EventTimer(["synth_frames", "reverb"])
     syn.timer = breakdown
     breakdown.enabled = True
     for _ in range(min(args.steps, 20)):
@@ -211,14 +211,14 @@ def main():
     traffic = load_traffic(args.traffic)
 
     # dominant kernel: fused oscillator (per-launch = B*F*bs samples of this rank)
-    osc_ms = timer.mean_ms("harmonic_synth")
+    osc_ms = timer.mean_ms("synth_frames")
     osc_bytes = 4 * (H + 2) * B * F * bs
     osc_gbs = osc_bytes / (osc_ms * 1e-3) / 1e9
     n_sin = B * F * bs * H
     roofline = {"bound": "hbm", "achieved": round(osc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(osc_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic.get("harmonic_frames_kernel"),
-                "kernel": "harmonic_frames_kernel<2,true> (HarmonicSynth.get_controls+forward fused)",
+                "kernel": "synth_frame_kernel (oscillator bank + filtered noise + their controls, fused)",
                 "algorithmic_bytes_per_launch": osc_bytes, "avg_launch_ms": round(osc_ms, 4),
                 "convention": "SURVEY 8(d): 4*(H+2) B/sample op-boundary bytes credited to the fused "
                               "kernel; it physically reads only frame-rate controls",

@@ -39,6 +39,8 @@ SIGNATURES = {
     "ddsp_hip_harmonic_synth_params": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_filtered_noise": (_I, [_P, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "ddsp_hip_filtered_noise_params": (_I, [_P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "ddsp_hip_synth_frames": (_I, [_P, _P, _P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64,
+                                   _I64, _F, _P]),
     "ddsp_hip_reverb_build_impulse": (_I, [_P, _P, _P, _P, _I64, _F, _P]),
     "ddsp_hip_reverb_spectrum_floats": (_SZ, [_I64, _I64]),
     "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
@@ -70,13 +72,16 @@ def load():
     return _lib
 
 
-def call(name, *args):
-    """Invoke ddsp_hip_<name>; map a non-zero status to RuntimeError."""
+def call(name, *args, allow=()):
+    """Invoke ddsp_hip_<name>; map a non-zero status (other than those in `allow`) to RuntimeError."""
     lib = load()
     st = getattr(lib, "ddsp_hip_" + name)(*args)
+    if st in allow:
+        return st
     if st != 0:
         msg = lib.ddsp_hip_status_string(st).decode()
         raise RuntimeError(f"ddsp_hip_{name} failed with status {st}: {msg}")
+    return 0
 
 
 def query(name, *args):

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
-    "harmonic_synth_frames", "harmonic_synth_params", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
+    "harmonic_synth_frames", "harmonic_synth_params", "synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
     "reverb_spectrum", "reverb_apply", "set_noise_seed",
 ]
 
@@ -308,6 +308,41 @@ def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=Fa
     if return_noise:
         return out, (nout if nout is not None else out)
     return out
+
+
+ERANGE = 5
+
+
+def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None, parts=False):
+    """decoder.py:106-121 in one kernel: raw harmonic projection param[B,F,H+1], pitch f0[B,F,1]
+    and raw noise projection mags[B,F,NB] -> signal = harmonic + noise [B,F*bs,1].
+
+    ``noise`` [B,F,bs] injects the U[-1,1) samples (else on-device Philox).  With ``parts`` the
+    harmonic and noise signals are returned too.  Returns None when the shape is outside the
+    fused kernel's envelope (block_size % 4 == 0 and <= 1024, H <= 1024, NB <= 1025)."""
+    _dev(f0, param, mags)
+    _no_grad_guard(f0, param, mags)
+    B, F, H1 = param.shape
+    NB = mags.shape[-1]
+    bs = int(block_size)
+    if f0.shape != (B, F, 1) or mags.shape[:2] != (B, F) or H1 < 2:
+        raise RuntimeError("synth_frames: f0 [B,F,1], param [B,F,H+1], mags [B,F,NB] expected")
+    f0c, pc, mc = _c(f0), _c(param), _c(mags)
+    if noise is not None:
+        _dev(noise)
+        if tuple(noise.shape) != (B, F, bs):
+            raise RuntimeError(f"synth_frames: noise must be [B, F, block_size] = {(B, F, bs)}")
+        noise = _c(noise)
+    out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=f0.device)
+    harm = torch.empty_like(out) if parts else None
+    nz = torch.empty_like(out) if parts else None
+    seed, offset = _noise_counter.next() if noise is None else (0, 0)
+    st = _lib.call("synth_frames", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
+                   seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), B, F, H1 - 1, NB, bs,
+                   float(sample_rate), _lib.stream_of(out), allow=(ERANGE,))
+    if st == ERANGE:
+        return None
+    return (out, harm, nz) if parts else out
 
 
 def reverb_build_impulse(noise, decay, wet, sample_rate):

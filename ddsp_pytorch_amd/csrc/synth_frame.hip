@@ -1,0 +1,242 @@
+// The synthesis section of DDSPDecoder.forward (decoder.py:106-121) for one frame in one
+// workgroup: harmonic controls + oscillator bank (modules.py:44-80), noise controls + filter
+// design + filtered noise (modules.py:111-128), and `signal = harmonic + noise`.
+//
+// Why fuse: the oscillator bank is VALU-bound (12 VALU ops per sample x harmonic) while the
+// filtered-noise work is short, LDS- and latency-heavy phases.  In one kernel the noise phases
+// of some workgroups run beside the sine loops of others on the same CU, the harmonic signal
+// never makes an HBM round trip, and one launch replaces two.
+//
+// Mapping: thread t owns samples [4t, 4t+4) of the frame for both parts (bs <= 1024,
+// bs % 4 == 0), so the harmonic and noise values of a sample meet in registers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "noise_dsp.h"
+
+namespace ddsp {
+namespace {
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Block-wide sums of two doubles (blockDim.x multiple of 64).
+__device__ __forceinline__ void block_sum_double2(double& a, double& b, double* scratch /*>=32*/) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64);
+    b += __shfl_down(b, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    scratch[2 * wid] = a;
+    scratch[2 * wid + 1] = b;
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    a += scratch[2 * i];
+    b += scratch[2 * i + 1];
+  }
+}
+
+template <bool RNG>
+__global__ void __launch_bounds__(256) synth_frame_kernel(
+    const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
+    float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
+    float* __restrict__ out, float* __restrict__ harm_out, float* __restrict__ noise_out, int F, int H,
+    int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
+  extern __shared__ float4 smem4[];
+  __shared__ double red[32];
+  const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
+  const int H4 = (H + 3) & ~3;
+  float4* coef = smem4;                                   // [2*H4] float4
+  float* ct = reinterpret_cast<float*>(coef + 2 * H4);    // [n4]
+  float* A = ct + n4;                                     // [NB -> 4]
+  float* ir = A + ((NB + 3) & ~3);                        // [half+1 -> 4]
+  float* h = ir + ((half + 4) & ~3);                      // [bs]
+  float* tail = h + bs;                                   // [half -> 4]
+  float* xbuf = tail + ((half + 3) & ~3);                 // [pad zeros | bs samples]
+  float* x = xbuf + pad;
+
+  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, NT = blockDim.x;
+  const int64_t frame = (int64_t)b * F + f;
+  const float* f0b = f0 + (int64_t)b * F;
+  const float* prow = param + frame * (H + 1);
+  const float half_sr = sr * 0.5f;
+  const float pitch0 = f0b[f];
+
+  // ---- phase 1: independent loads and per-element work ----
+  double part_s = 0.0, part_d = 0.0;
+  for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
+  for (int k = tid; k < H; k += NT) {  // modules.py:53-60 before normalisation
+    const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+    coef[2 * k].x = v;
+    part_d += (double)v;
+  }
+  for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * NB + k] + bias);  // modules.py:113
+  fill_cos_table(ct, n);
+  for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
+  const int quads = bs >> 2;
+  for (int t = tid; t < quads; t += NT) {
+    float4 v;
+    if (RNG) {
+      const uint64_t q = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
+      const Philox4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
+      v = make_float4(uniform_pm1(r.v[0]), uniform_pm1(r.v[1]), uniform_pm1(r.v[2]), uniform_pm1(r.v[3]));
+    } else {
+      v = *reinterpret_cast<const float4*>(noise + frame * bs + 4 * t);
+    }
+    *reinterpret_cast<float4*>(x + 4 * t) = v;
+  }
+  block_sum_double2(part_s, part_d, red);  // includes the barrier that publishes phase 1
+  const double S = part_s;                 // exact fp64 prefix over earlier frames
+  const float norm = (float)part_d;        // dist.sum(-1)
+  const float a = scale_fn(prow[0]);
+
+  // ---- phase 2: harmonic coefficient table; even half of the noise filter taps ----
+  for (int k = tid; k < H4; k += NT) {
+    const float v = k < H ? (coef[2 * k].x / norm) * a : 0.0f;  // (dist / sum) * amp
+    coef[2 * k] = make_float4(v, v * kS3, v * kS5, v * kS7);
+    coef[2 * k + 1] = make_float4(v * kS9, (float)(k + 1), v, 0.0f);
+  }
+  if (n == 128 && NT >= 128) {
+    if (tid < 64) {
+      const int m = tid;
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 8
+      for (int k = 1; k < 63; k += 2) {
+        s0 = fmaf(A[k], kIrCos128[k * 64 + m], s0);
+        s1 = fmaf(A[k + 1], kIrCos128[(k + 1) * 64 + m], s1);
+      }
+      s0 = fmaf(A[63], kIrCos128[63 * 64 + m], s0);
+      ir[m] = (A[0] + ((m & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
+    } else if (tid < 128) {  // tap n/2: cos(pi k) = (-1)^k
+      float alt = (tid - 64 >= 1 && tid - 64 < 64) ? (((tid - 64) & 1) ? -A[tid - 64] : A[tid - 64]) : 0.0f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
+      if (tid == 64) ir[64] = (A[0] + A[64] + 2.0f * alt) * (1.0f / 128.0f);
+    }
+  } else {
+    for (int m = tid; m <= half; m += NT) ir[m] = irfft_tap(A, ct, n, m);
+  }
+  __syncthreads();
+
+  // ---- phase 3: rolled/windowed filter h (core.py:158-164) ----
+  for (int j = tid; j < bs; j += NT) h[j] = ir_at_half(ir, ct, n, bs, j);
+  __syncthreads();
+
+  // ---- phase 4: noise tail (taps past bs - n/2 reach only the last n/2 outputs) ----
+  for (int l = tid; l < bs - tail_start; l += NT) {
+    const int j = tail_start + l;
+    float c = 0.0f;
+    for (int d = 0; d <= l; ++d) c = fmaf(h[j - d], x[d], c);
+    tail[l] = c;
+  }
+
+  // ---- phase 5: oscillator bank for samples [j0, j0+4) ----
+  const int j0 = 4 * tid;
+  const bool active = j0 < bs;
+  const double dinc = (double)phase_inc(pitch0, sr);
+  float w[4], acc[4];
+  bool fast = true;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w[s] = (float)(S + (double)(j0 + s + 1) * dinc);  // omega = fl32(exact prefix)
+    acc[s] = 0.0f;
+    fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
+  }
+  if (active) {
+    if (fast) {
+#pragma unroll 2
+      for (int k = 0; k < H4; ++k) {
+        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
+      }
+    } else {
+      for (int k = 0; k < H; ++k) {
+        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float xx = w[s] * c1.y;
+          acc[s] = fabsf(xx) < kFastArgLimit
+                       ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
+                       : fmaf(sin_slow(xx), c1.z, acc[s]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // tail[] complete
+  if (!active) return;
+
+  // ---- phase 6: filtered noise for the same samples, sum, store ----
+  float4 y = fir4(h, x, j0, lo_end, bs, bs);  // taps [0, lo_end); the wrapped taps are in tail[]
+  float nz[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if (j0 + s >= tail_start) nz[s] += tail[j0 + s - tail_start];
+  const int64_t o = frame * bs + j0;
+  if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (noise_out) *reinterpret_cast<float4*>(noise_out + o) = make_float4(nz[0], nz[1], nz[2], nz[3]);
+  *reinterpret_cast<float4*>(out + o) =
+      make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121
+}
+
+}  // namespace
+}  // namespace ddsp
+
+using namespace ddsp;
+
+extern "C" {
+
+int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                          const float* noise, uint64_t seed, uint64_t offset, float* out,
+                          float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
+                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                          void* stream) {
+  if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
+  if (!f0 || !param || !raw_magnitudes || !out) return DDSP_HIP_EINVAL;
+  // the fused kernel's shape envelope; callers fall back to the separate kernels outside it
+  if (block_size % 4 || block_size > 1024 || n_harmonic > 1024 || n_bands > 1025 || batch > 65535 ||
+      frames > INT32_MAX)
+    return DDSP_HIP_ERANGE;
+  const int n = 2 * (int)(n_bands - 1), half = n / 2, bs = (int)block_size;
+  int lo_end, tail_start;
+  if (bs >= n) {
+    lo_end = (half + 3) & ~3;
+    tail_start = bs - half;
+    if (tail_start < lo_end) {
+      lo_end = bs;
+      tail_start = bs;
+    }
+  } else {
+    lo_end = bs;
+    tail_start = bs;
+  }
+  const int pad = (lo_end + 4 + 3) & ~3;
+  const int H4 = ((int)n_harmonic + 3) & ~3, n4 = (n + 3) & ~3;
+  const size_t floats = (size_t)8 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs +
+                        ((half + 3) & ~3) + pad + bs;
+  const size_t shm = sizeof(float) * floats;
+  if (shm > 120 * 1024) return DDSP_HIP_ERANGE;
+  const int nt = std::max(64, ((bs / 4 + 63) / 64) * 64);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
+  const dim3 grid((unsigned)frames, (unsigned)batch);
+  if (noise)
+    hipLaunchKernelGGL(synth_frame_kernel<false>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
+                       bias, noise, k0, k1, o0, o1, out, harmonic_out, noise_out, (int)frames,
+                       (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
+  else
+    hipLaunchKernelGGL(synth_frame_kernel<true>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
+                       bias, nullptr, k0, k1, o0, o1, out, harmonic_out, noise_out, (int)frames,
+                       (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
+  return launch_status();
+}
+
+}  // extern "C"

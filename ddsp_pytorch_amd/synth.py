@@ -3,8 +3,8 @@ frame-rate controls -> harmonic + filtered noise -> reverb -> audio.
 
 This is the unit the benchmark times (SURVEY.md §8(d) "End-to-end unit"): raw
 harmonic parameters [B,F,H+1], pitch [B,F,1] and raw noise magnitudes [B,F,NB] in,
-audio [B,F*bs,1] out.  Kernels per call: oscillator bank fused with its controls,
-fused filtered noise with its controls (+ harmonic sum), reverb (partitioned FFT).
+audio [B,F*bs,1] out.  Kernels per call: one synthesis-frame kernel (both synths, their controls, the sum)
+and the reverb (partitioned FFT convolution: forward, MAC, inverse).
 """
 import torch
 import torch.nn as nn
@@ -54,19 +54,17 @@ class SynthPath(nn.Module):
 
     @torch.no_grad()
     def forward(self, f0, param, mags, noise=None):
-        # HarmonicSynth.get_controls + forward (modules.py:44-80) in one kernel
-        with self._t("harmonic_synth"):
-            harmonic = core.harmonic_synth_params(f0, param, self.block_size, self.sample_rate)
-        # FilteredNoise.get_controls + forward (modules.py:111-128) + `harmonic + noise`
-        # (decoder.py:121) in one kernel
-        with self._t("filtered_noise"):
-            if self.noise_mode == "inject":
-                if noise is None:
-                    raise ValueError("noise_mode='inject' needs a noise tensor")
-                signal = core.filtered_noise(mags, self.block_size, noise=noise, add=harmonic,
-                                             raw_bias=self.initial_bias)
-            else:
-                signal = core.filtered_noise(mags, self.block_size, add=harmonic,
+        if self.noise_mode == "inject" and noise is None:
+            raise ValueError("noise_mode='inject' needs a noise tensor")
+        nz = noise if self.noise_mode == "inject" else None
+        # decoder.py:106-121 (both synths, their controls and the sum) in one kernel
+        with self._t("synth_frames"):
+            signal = core.synth_frames(f0, param, mags, self.block_size, self.sample_rate,
+                                       bias=self.initial_bias, noise=nz)
+        if signal is None:  # outside the fused kernel's envelope: two kernels
+            with self._t("synth_frames"):
+                harmonic = core.harmonic_synth_params(f0, param, self.block_size, self.sample_rate)
+                signal = core.filtered_noise(mags, self.block_size, noise=nz, add=harmonic,
                                              raw_bias=self.initial_bias)
         if self.reverb is not None:
             with self._t("reverb"):

@@ -128,6 +128,18 @@ int ddsp_hip_filtered_noise_params(const float* raw_magnitudes, float bias, cons
                                    float* noise_out, int64_t batch, int64_t frames, int64_t n_bands,
                                    int64_t block_size, void* stream);
 
+/* decoder.py:106-121 in one launch: HarmonicSynth.get_controls + forward from the harmonic
+ * projection param[B,F,H+1], FilteredNoise.get_controls + forward from the raw noise projection
+ * raw_magnitudes[B,F,NB] (scale_function(x + bias)), and signal = harmonic + noise -> out[B,F*bs].
+ * noise / seed / offset as ddsp_hip_filtered_noise; harmonic_out and noise_out (nullable)
+ * receive the two parts.  Shape envelope: block_size % 4 == 0 and <= 1024, H <= 1024,
+ * NB <= 1025; outside it DDSP_HIP_ERANGE is returned and callers use the separate kernels. */
+int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                          const float* noise, uint64_t seed, uint64_t offset, float* out,
+                          float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
+                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                          void* stream);
+
 /* modules.py:21-26  Reverb.build_impulse: noise[L]*exp(-softplus(-decay)*t*500)*sigmoid(wet),
  * impulse[0] = 1.  decay and wet are device scalars. */
 int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const float* wet,

@@ -338,3 +338,29 @@ def test_config5_synth_path_items(dd):
         ref = tr.synth_path(inp["f0"][sl].cpu(), inp["param"][sl].cpu(), inp["mags"][sl].cpu(),
                             inp["noise"][sl].cpu(), rv, 512, 48000)
         assert rms(C(out[sl]), ref.numpy()) < PARITY_RMS
+
+
+# ------------------------------------------------------------------ fused synthesis frame
+@pytest.mark.parametrize("B,F,H,NB,bs", [(2, 16, 100, 65, 512), (1, 6, 64, 65, 256), (2, 5, 17, 9, 64),
+                                         (1, 3, 128, 129, 1024), (1, 4, 100, 65, 441)])
+def test_synth_frames_vs_oracle(dd, B, F, H, NB, bs):
+    """decoder.py:106-121 in one kernel (or the two-kernel fallback outside its envelope)."""
+    rng = np.random.default_rng(B * 100 + H + bs)
+    f0 = (50.0 * 20.0 ** rng.random((B, F, 1))).astype(np.float32)
+    param = rng.standard_normal((B, F, H + 1)).astype(np.float32)
+    mags = rng.standard_normal((B, F, NB)).astype(np.float32)
+    noise = (rng.random((B, F, bs)) * 2 - 1).astype(np.float32)
+    c = no.harmonic_get_controls(param[..., :1], param[..., 1:], f0, 48000)
+    harm_ref, _ = no.harmonic_forward(c["amplitudes"], c["harmonic_distribution"], f0, bs, 48000)
+    noise_ref = no.noise_forward(no.noise_get_controls(mags)["magnitudes"], noise, bs)
+    with torch.no_grad():
+        r = dd.core.synth_frames(G(f0), G(param), G(mags), bs, 48000, noise=G(noise), parts=True)
+        syn = dd.synth.SynthPath(bs, 48000, reverb_length=None, noise_mode="inject")
+        path = C(syn(G(f0), G(param), G(mags), G(noise)))
+    if bs % 4:
+        assert r is None  # outside the fused envelope
+    else:
+        out, harm, nz = (C(t) for t in r)
+        assert rms(harm, harm_ref) < 1e-6 and rms(nz, noise_ref) < 1e-7, (rms(harm, harm_ref), rms(nz, noise_ref))
+        assert rms(out, harm_ref + noise_ref) < 1e-6
+    assert rms(path, harm_ref + noise_ref) < 1e-6
