@@ -200,8 +200,10 @@ __global__ void __launch_bounds__(kNT) upols_kernel_spectrum_kernel(const float*
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
 }
 
-// Y[pair][b][f] = sum_p X[pair][b-p][f] * H[p][f]; each thread one bin, 8 consecutive blocks.
-// grid (N/256, ceil(nb/8), npairs)
+// Y[pair][b][f] = sum_p X[pair][b-p][f] * H[p][f]; each thread one bin, BLK consecutive blocks
+// with a sliding window of X in registers.  grid (N/256, ceil(nb/BLK), npairs)
+// (Measured: a register double-buffered prefetch of the next partitions ran 5-10% slower — the
+// extra registers cost more occupancy than the hidden latency bought.)
 template <int BLK>
 __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict__ X,
                                                         const float2* __restrict__ Hs,
@@ -212,11 +214,14 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
   const int pair = blockIdx.z;
   const float2* Xp = X + (int64_t)pair * nb * kN + f;
   const float2* Hp = Hs + (int64_t)pair * h_pair_stride + f;
+  const float2 zero = make_float2(0.f, 0.f);
   float2 acc[BLK], win[BLK];
 #pragma unroll
   for (int d = 0; d < BLK; ++d) {
-    acc[d] = make_float2(0.f, 0.f);
-    win[d] = (b0 + d < nb) ? Xp[(int64_t)(b0 + d) * kN] : make_float2(0.f, 0.f);
+    acc[d] = zero;
+    // clamped load + value select (a select of pointers made hipcc go through scratch)
+    const float2 xv = Xp[(int64_t)min(b0 + d, nb - 1) * kN];
+    win[d] = b0 + d < nb ? xv : zero;
   }
   const int pmax = min(Q, b0 + BLK);
 #pragma unroll 4
@@ -230,7 +235,8 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
 #pragma unroll
     for (int d = BLK - 1; d > 0; --d) win[d] = win[d - 1];
     const int bn = b0 - p - 1;
-    win[0] = bn >= 0 ? Xp[(int64_t)bn * kN] : make_float2(0.f, 0.f);
+    const float2 xv = Xp[(int64_t)max(bn, 0) * kN];
+    win[0] = bn >= 0 ? xv : zero;
   }
   float2* Yp = Y + (int64_t)pair * nb * kN + f;
 #pragma unroll

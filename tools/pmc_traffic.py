@@ -21,6 +21,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WIDE_READS = ("harmonic_samples_tiled_kernel",)  # 16-B/lane streaming amplitude reads
 REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch of it
+    "synth_frame_kernel": ("synth_frame_kernel",),
     "harmonic_frames_kernel": ("harmonic_frames_kernel",),
     "harmonic_samples_kernel": ("phase_chunk_sums_kernel", "harmonic_samples_tiled_kernel"),
     "filtered_noise_kernel": ("filtered_noise_kernel",),
@@ -61,7 +62,8 @@ def main():
                     "hbm_bytes": int((f_kib * corr + w_kib) * 1024)}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(table, f, indent=1)
-    traffic = {key: sum(table[k]["hbm_bytes"] for k in ks if k in table) for key, ks in REPORT.items()}
+    traffic = {key: sum(table[k]["hbm_bytes"] for k in ks if k in table) for key, ks in REPORT.items()
+               if any(k in table for k in ks)}
     traffic["_source"] = f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
