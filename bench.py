@@ -57,9 +57,11 @@ def parse():
     p.add_argument("--noise", choices=("device", "inject"), default="device")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-op-leg", action="store_true")
-    p.add_argument("--gather", action="store_true",
-                   help="N>1: also time synth + RCCL gather of the audio to rank 0 (reported "
-                        "separately as 'gathered'; value stays the sharded throughput)")
+    p.add_argument("--no-gather", action="store_true",
+                   help="N>1: skip the synth + RCCL gather-to-rank-0 leg (reported separately as "
+                        "'gathered'; value is always the left-sharded throughput)")
+    p.add_argument("--no-decoder-leg", action="store_true",
+                   help="skip the full DDSPDecoder.forward leg (GRU/MLP + synthesis)")
     p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -144,6 +146,35 @@ def cpu_baseline(args, rank_inputs_seed=0):
                       f"config {args.config} (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
                       f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {len(times)} runs, "
                       f"{t:.3f} s each"}
+
+
+def decoder_leg(args, inp, dev, reps=10):
+    """the full DDSPDecoder.forward rate, reported beside the synthesis path —
+    GRU/MLP control network (hidden 512, torch on MIOpen/hipBLASLt) + the gfx950 synthesis."""
+    from ddsp_pytorch_amd.decoder import DDSPDecoder
+    B, F = args.batch, args.frames
+    torch.manual_seed(0)
+    model = DDSPDecoder(512, args.harmonics, args.bands, args.sample_rate, args.block_size, True)
+    model = model.to(dev).eval()
+    model.noise_synth.noise_mode = "device"
+    if args.reverb_length != args.sample_rate:
+        model.reverb = type(model.reverb)(args.reverb_length, args.sample_rate).to(dev)
+    batch = {"pitch": inp["f0"], "loudness": torch.randn(B, F, 1, device=dev)}
+    with torch.no_grad():
+        for _ in range(3):
+            model(batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = model(batch)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+    assert torch.isfinite(out["signal"]).all()
+    del model
+    return {"value": round(B * F * args.block_size / t, 1), "unit": "samples/s",
+            "ms_per_forward": round(t * 1e3, 4),
+            "model": f"DDSPDecoder(hidden 512, H {args.harmonics}, NB {args.bands}, reverb "
+                     f"{args.reverb_length}), random init, batch {B} x {F} frames"}
 
 
 def main():
@@ -243,7 +274,7 @@ def main():
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
     }
 
-    if dist and args.gather:
+    if dist and not args.no_gather:
         from ddsp_pytorch_amd.shard import gather_audio
         torch.cuda.synchronize()
         dist.barrier()
@@ -282,6 +313,9 @@ def main():
                                  "traffic": traffic.get("harmonic_samples_kernel"),
                                  "kernel": "phase_chunk_sums_kernel + harmonic_samples_kernel<true>",
                                  "avg_launch_ms": round(op_ms, 4)}
+
+    if rank == 0 and not args.no_decoder_leg:
+        result["decoder_forward"] = decoder_leg(args, inp, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
