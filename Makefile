@@ -3,7 +3,8 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 SRC := ddsp_pytorch_amd/csrc/synth.hip ddsp_pytorch_amd/csrc/noise.hip ddsp_pytorch_amd/csrc/reverb.hip \
-       ddsp_pytorch_amd/csrc/upols.hip ddsp_pytorch_amd/csrc/synth_frame.hip
+       ddsp_pytorch_amd/csrc/upols.hip ddsp_pytorch_amd/csrc/synth_frame.hip \
+       ddsp_pytorch_amd/csrc/backward.hip
 HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h ddsp_pytorch_amd/csrc/upols.h \
        ddsp_pytorch_amd/csrc/noise_dsp.h
 LIB := ddsp_pytorch_amd/lib/libddsp_hip.so
@@ -11,6 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 # packed-fp32 SLP vectorisation measured 10% slower on the oscillator loop (VALU-bound)
 HIPFLAGS_synth := -fno-slp-vectorize
 HIPFLAGS_synth_frame := -fno-slp-vectorize
+HIPFLAGS_backward := -fno-slp-vectorize
 OBJ := $(patsubst ddsp_pytorch_amd/csrc/%.hip,build/%.o,$(SRC))
 
 TORCH_DIR := $(shell python3 -c "import torch,os;print(os.path.dirname(torch.__file__))" 2>/dev/null)
@@ -24,7 +26,7 @@ build/twiddle4096.inc: tools/gen_twiddles.py
 	@mkdir -p build
 	python3 tools/gen_twiddles.py 4096 > $@
 
-build/upols.o build/noise.o build/synth_frame.o: build/twiddle4096.inc
+build/upols.o build/noise.o build/synth_frame.o build/backward.o: build/twiddle4096.inc
 
 build/%.o: ddsp_pytorch_amd/csrc/%.hip $(HDR)
 	@mkdir -p build

@@ -44,10 +44,9 @@ def _dev(*tensors):
     return dev
 
 
-def _no_grad_guard(*tensors):
-    if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
-        raise RuntimeError("ddsp_hip: backward kernels are not implemented yet; "
-                           "call under torch.no_grad() / inference_mode()")
+def _wants_grad(*tensors):
+    """autograd must record this call: dispatch to the Function in grad.py (backward kernels)."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
 
 
 def _c(t):
@@ -73,7 +72,8 @@ def scale_function(x):
 def scale_with_bias(x, bias):
     """``scale_function(x + bias)`` in one kernel (FilteredNoise.get_controls, modules.py:111-114)."""
     _dev(x)
-    _no_grad_guard(x)
+    if _wants_grad(x):
+        return _grad.ScaleFn.apply(x, float(bias))
     x = _c(x)
     y = torch.empty_like(x)
     _lib.call("scale_function", _lib.ptr(x), _lib.ptr(y), x.numel(), float(bias), _lib.stream_of(x))
@@ -83,7 +83,8 @@ def scale_with_bias(x, bias):
 def remove_above_nyquist(amplitudes, f0, sample_rate):
     """ddsp/core.py:70-74  amplitudes[..., H] * ((f0 * k < sr/2) + 1e-4), k = 1..H."""
     _dev(amplitudes, f0)
-    _no_grad_guard(amplitudes, f0)
+    if _wants_grad(amplitudes, f0):
+        return _grad.NyquistFn.apply(amplitudes, f0, sample_rate)
     H = amplitudes.shape[-1]
     lead = amplitudes.shape[:-1]
     if f0.shape[-1] != 1:
@@ -101,7 +102,8 @@ def remove_above_nyquist(amplitudes, f0, sample_rate):
 def upsample(signal, factor):
     """ddsp/core.py:64-67  nearest upsampling [B, F, C] -> [B, F*factor, C]."""
     _dev(signal)
-    _no_grad_guard(signal)
+    if _wants_grad(signal):
+        return _grad.UpsampleFn.apply(signal, int(factor))
     if signal.dim() != 3:
         raise RuntimeError(f"upsample: expected [batch, frames, channels], got {tuple(signal.shape)}")
     factor = int(factor)
@@ -115,7 +117,9 @@ def upsample(signal, factor):
 def harmonic_synth(f0, amplitudes, sample_rate):
     """ddsp/core.py:136-141  f0[B, T, 1], amplitudes[B, T, H] -> [B, T, 1]."""
     _dev(f0, amplitudes)
-    _no_grad_guard(f0, amplitudes)
+    if _wants_grad(f0, amplitudes):
+        _grad.refuse_f0_grad(f0, "harmonic_synth")
+        return _grad.HarmonicSynthFn.apply(f0, amplitudes, sample_rate)
     if amplitudes.dim() != 3 or f0.dim() != 3 or f0.shape[-1] != 1:
         raise RuntimeError("harmonic_synth: expected f0 [B,T,1] and amplitudes [B,T,H], got "
                            f"{tuple(f0.shape)} and {tuple(amplitudes.shape)}")
@@ -147,7 +151,8 @@ def phase(f0, sample_rate):
 def amp_to_impulse_response(amp, target_size):
     """ddsp/core.py:144-166  zero-phase FIR of length target_size from NB magnitudes."""
     _dev(amp)
-    _no_grad_guard(amp)
+    if _wants_grad(amp):
+        return _grad.ImpulseResponseFn.apply(amp, int(target_size))
     NB = amp.shape[-1]
     if NB < 2:
         raise RuntimeError("amp_to_impulse_response: need at least 2 frequency bands")
@@ -163,7 +168,8 @@ def amp_to_impulse_response(amp, target_size):
 def fft_convolve(signal, kernel):
     """ddsp/core.py:169-176  causal linear convolution truncated to N (last dim), with broadcasting."""
     _dev(signal, kernel)
-    _no_grad_guard(signal, kernel)
+    if _wants_grad(signal, kernel):
+        return _grad.FFTConvolveFn.apply(signal, kernel)
     N = signal.shape[-1]
     if kernel.shape[-1] != N:
         raise RuntimeError(f"fft_convolve: signal and kernel lengths differ ({N} vs {kernel.shape[-1]})")
@@ -194,7 +200,9 @@ def _rows_view(t, name):
 def harmonic_controls(amplitudes, harmonic_distribution, f0, sample_rate):
     """modules.py:44-67 HarmonicSynth.get_controls, fused: returns (amplitudes, distribution)."""
     _dev(amplitudes, harmonic_distribution, f0)
-    _no_grad_guard(amplitudes, harmonic_distribution, f0)
+    if _wants_grad(amplitudes, harmonic_distribution, f0):
+        _grad.refuse_f0_grad(f0, "harmonic_controls")
+        return _grad.ControlsFn.apply(amplitudes, harmonic_distribution, f0, sample_rate)
     B, F, H = harmonic_distribution.shape
     if amplitudes.shape != (B, F, 1) or f0.shape != (B, F, 1):
         raise RuntimeError("harmonic_controls: expected amplitudes/f0 [B,F,1] matching "
@@ -220,7 +228,12 @@ def harmonic_synth_frames(f0, amplitudes, harmonic_distribution, block_size, sam
     (modules.py:73), which the reference's caller sees through its controls dict.
     """
     _dev(f0, amplitudes, harmonic_distribution)
-    _no_grad_guard(f0, amplitudes, harmonic_distribution)
+    if _wants_grad(f0, amplitudes, harmonic_distribution):
+        _grad.refuse_f0_grad(f0, "harmonic_synth_frames")
+        out = _grad.SynthFramesHarmonicFn.apply(f0, amplitudes, harmonic_distribution, block_size, sample_rate)
+        if write_back:  # modules.py:73, recorded by autograd like the reference's in-place multiply
+            harmonic_distribution.mul_(amplitudes)
+        return out
     B, F, H = harmonic_distribution.shape
     f0c, ac = _c(f0), _c(amplitudes)
     dist = harmonic_distribution
@@ -260,7 +273,9 @@ def harmonic_synth_params(f0, param, block_size, sample_rate):
     param[B, F, H+1] (column 0 amplitude, 1..H distribution) and f0 [B, F, 1] -> audio
     [B, F*block_size, 1].  The controls (scale, Nyquist mask, normalisation) never reach HBM."""
     _dev(f0, param)
-    _no_grad_guard(f0, param)
+    if _wants_grad(f0, param):
+        _grad.refuse_f0_grad(f0, "harmonic_synth_params")
+        return _grad.HarmonicParamsFn.apply(f0, param, block_size, sample_rate)
     B, F, H1 = param.shape
     if f0.shape != (B, F, 1) or H1 < 2:
         raise RuntimeError(f"harmonic_synth_params: f0 {tuple(f0.shape)} / param {tuple(param.shape)}")
@@ -275,14 +290,28 @@ def harmonic_synth_params(f0, param, block_size, sample_rate):
 def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=False, raw_bias=None):
     """modules.py:116-128 FilteredNoise.forward, fused.
 
-    magnitudes: [B, F, NB] (already scaled by get_controls).  ``noise`` [B, F, block_size]
-    injects the U[-1,1) samples (parity mode, e.g. the reference's ``torch.rand`` stream);
-    ``None`` draws them on the device with Philox4x32-10.  ``add`` [B, F*bs, 1] is added to
-    the result (fuses ``harmonic + noise``); with ``return_noise`` the filtered noise alone is
-    returned as a second tensor.
+    magnitudes: [B, F, NB] (already scaled by get_controls; with ``raw_bias`` the raw
+    projection, scaled in the kernel as scale_function(x + raw_bias)).  ``noise``
+    [B, F, block_size] injects the U[-1,1) samples (parity mode, e.g. the reference's
+    ``torch.rand`` stream); ``None`` draws them on the device with Philox4x32-10.  ``add``
+    [B, F*bs, 1] is added to the result (fuses ``harmonic + noise``); with ``return_noise`` the
+    filtered noise alone is returned as a second tensor.
     """
     _dev(magnitudes)
-    _no_grad_guard(magnitudes)
+    if _wants_grad(magnitudes, add):
+        outs = _grad.FilteredNoiseFn.apply(magnitudes, add, int(block_size), noise, raw_bias,
+                                           bool(return_noise))
+        if return_noise and not isinstance(outs, tuple):
+            return outs, outs
+        return outs
+    seed, offset = _noise_counter.next() if noise is None else (0, 0)
+    out = _filtered_noise_launch(magnitudes, block_size, noise, add, return_noise, raw_bias, seed, offset)
+    if return_noise and not isinstance(out, tuple):
+        return out, out
+    return out
+
+
+def _filtered_noise_launch(magnitudes, block_size, noise, add, return_noise, raw_bias, seed, offset):
     B, F, NB = magnitudes.shape
     bs = int(block_size)
     m = _c(magnitudes)
@@ -298,19 +327,35 @@ def filtered_noise(magnitudes, block_size, noise=None, add=None, return_noise=Fa
             raise RuntimeError("filtered_noise: `add` must have B*F*block_size elements")
     out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=m.device)
     nout = torch.empty_like(out) if (return_noise and add is not None) else None
-    seed, offset = _noise_counter.next() if noise is None else (0, 0)
     if raw_bias is None:
         _lib.call("filtered_noise", _lib.ptr(m), _lib.ptr(noise), seed, offset, _lib.ptr(add),
                   _lib.ptr(out), _lib.ptr(nout), B, F, NB, bs, _lib.stream_of(m))
     else:
         _lib.call("filtered_noise_params", _lib.ptr(m), float(raw_bias), _lib.ptr(noise), seed, offset,
                   _lib.ptr(add), _lib.ptr(out), _lib.ptr(nout), B, F, NB, bs, _lib.stream_of(m))
-    if return_noise:
-        return out, (nout if nout is not None else out)
-    return out
+    return (out, nout) if nout is not None else out
 
 
 ERANGE = 5
+
+
+def synth_frames_in_envelope(n_harmonic, n_bands, block_size, batch=1):
+    """The fused kernel's shape envelope (mirrors ddsp_hip_synth_frames' DDSP_HIP_ERANGE checks)."""
+    H, NB, bs = int(n_harmonic), int(n_bands), int(block_size)
+    if bs % 4 or bs > 1024 or H > 1024 or NB > 1025 or batch > 65535:
+        return False
+    n = 2 * (NB - 1)
+    half = n // 2
+    if bs >= n:
+        lo_end, tail_start = (half + 3) & ~3, bs - half
+        if tail_start < lo_end:
+            lo_end = bs
+    else:
+        lo_end = bs
+    pad = (lo_end + 4 + 3) & ~3
+    H4, n4 = (H + 3) & ~3, (n + 3) & ~3
+    floats = 8 * H4 + n4 + ((NB + 3) & ~3) + ((half + 4) & ~3) + bs + ((half + 3) & ~3) + pad + bs
+    return 4 * floats <= 120 * 1024
 
 
 def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None, parts=False):
@@ -321,12 +366,24 @@ def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None
     harmonic and noise signals are returned too.  Returns None when the shape is outside the
     fused kernel's envelope (block_size % 4 == 0 and <= 1024, H <= 1024, NB <= 1025)."""
     _dev(f0, param, mags)
-    _no_grad_guard(f0, param, mags)
     B, F, H1 = param.shape
     NB = mags.shape[-1]
     bs = int(block_size)
     if f0.shape != (B, F, 1) or mags.shape[:2] != (B, F) or H1 < 2:
         raise RuntimeError("synth_frames: f0 [B,F,1], param [B,F,H+1], mags [B,F,NB] expected")
+    if not synth_frames_in_envelope(H1 - 1, NB, bs, B):
+        return None
+    if _wants_grad(f0, param, mags):
+        _grad.refuse_f0_grad(f0, "synth_frames")
+        return _grad.SynthFramesFn.apply(f0, param, mags, bs, float(sample_rate), float(bias), noise, bool(parts))
+    seed, offset = _noise_counter.next() if noise is None else (0, 0)
+    return _synth_frames_launch(f0, param, mags, bs, sample_rate, bias, noise, parts, seed, offset)
+
+
+def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, parts, seed, offset):
+    B, F, H1 = param.shape
+    NB = mags.shape[-1]
+    bs = int(block_size)
     f0c, pc, mc = _c(f0), _c(param), _c(mags)
     if noise is not None:
         _dev(noise)
@@ -336,18 +393,17 @@ def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None
     out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=f0.device)
     harm = torch.empty_like(out) if parts else None
     nz = torch.empty_like(out) if parts else None
-    seed, offset = _noise_counter.next() if noise is None else (0, 0)
-    st = _lib.call("synth_frames", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
-                   seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), B, F, H1 - 1, NB, bs,
-                   float(sample_rate), _lib.stream_of(out), allow=(ERANGE,))
-    if st == ERANGE:
-        return None
+    _lib.call("synth_frames", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
+              seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), B, F, H1 - 1, NB, bs,
+              float(sample_rate), _lib.stream_of(out))
     return (out, harm, nz) if parts else out
 
 
 def reverb_build_impulse(noise, decay, wet, sample_rate):
     """modules.py:21-26 Reverb.build_impulse: noise[L,1] -> impulse [1, L, 1]."""
     _dev(noise, decay, wet)
+    if _wants_grad(noise, decay, wet):
+        return _grad.BuildImpulseFn.apply(noise, decay, wet, sample_rate)
     L = noise.shape[0]
     n = _c(noise)
     imp = torch.empty(1, L, 1, dtype=torch.float32, device=n.device)
@@ -373,7 +429,11 @@ def reverb_spectrum(impulse, n_samples):
 def reverb_apply(x, spectrum, ir_length):
     """modules.py:28-35 Reverb.forward given the cached IR spectrum: x [B, T, 1] -> [B, T, 1]."""
     _dev(x, spectrum)
-    _no_grad_guard(x)
+    if _wants_grad(x, spectrum):
+        if spectrum.requires_grad:
+            raise NotImplementedError("reverb_apply: the IR spectrum is not differentiable; use "
+                                      "modules.Reverb (gradients for noise/decay/wet) instead")
+        return _grad.ReverbApplyFn.apply(x, spectrum, int(ir_length))
     B, T = x.shape[0], x.shape[1]
     if spectrum.numel() != reverb_spectrum_floats(T, ir_length):
         raise RuntimeError("reverb_apply: spectrum was computed for a different length")
@@ -383,3 +443,6 @@ def reverb_apply(x, spectrum, ir_length):
     _lib.call("reverb_apply", _lib.ptr(xc), _lib.ptr(spectrum), _lib.ptr(out), B, T, int(ir_length),
               _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
     return out
+
+
+from . import grad as _grad  # noqa: E402  (autograd Functions over the backward kernels)

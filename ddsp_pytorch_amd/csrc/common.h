@@ -145,6 +145,27 @@ __device__ __forceinline__ double block_sum_double(double v, double* scratch /*>
   return s;
 }
 
+// Block-wide sums of two doubles (blockDim.x multiple of 64).
+__device__ __forceinline__ void block_sum_double2(double& a, double& b, double* scratch /*>=32*/) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64);
+    b += __shfl_down(b, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    scratch[2 * wid] = a;
+    scratch[2 * wid + 1] = b;
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    a += scratch[2 * i];
+    b += scratch[2 * i + 1];
+  }
+}
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;

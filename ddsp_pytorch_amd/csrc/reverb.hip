@@ -46,6 +46,36 @@ __global__ void build_impulse_kernel(const float* __restrict__ noise, const floa
   }
 }
 
+// Reverb.build_impulse backward (modules.py:21-26): imp[i] = noise[i] env[i] w (i >= 1),
+// env = exp(-softplus(-decay) t 500), w = sigmoid(wet); imp[0] = 1 carries no gradient.
+// Taps i >= grad_len (cropped away by a shorter input) have zero gradient.  One workgroup.
+__global__ void __launch_bounds__(1024) impulse_backward_kernel(
+    const float* __restrict__ noise, const float* __restrict__ decay, const float* __restrict__ wet,
+    const float* __restrict__ dimp, int64_t grad_len, int64_t L, float sr, float* __restrict__ d_noise,
+    float* __restrict__ d_decay, float* __restrict__ d_wet) {
+  __shared__ double red[32];
+  const float d = -decay[0];
+  const float sp = d > 20.0f ? d : log1pf(expf(d));
+  const float spg = d > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-d));  // softplus'(d)
+  const float neg = -sp;
+  const float w = 1.0f / (1.0f + expf(-wet[0]));
+  double aw = 0.0, ad = 0.0;
+  for (int64_t i = threadIdx.x; i < L; i += blockDim.x) {
+    const float t = (float)i / sr;
+    const float env = expf((neg * t) * 500.0f);
+    const float gi = (i >= 1 && i < grad_len) ? dimp[i] : 0.0f;
+    d_noise[i] = gi * env * w;
+    const float gne = gi * noise[i] * env;
+    aw += (double)gne;
+    ad += (double)gne * (double)t;
+  }
+  block_sum_double2(aw, ad, red);
+  if (threadIdx.x == 0) {
+    d_wet[0] = (float)(aw * (double)w * (1.0 - (double)w));
+    d_decay[0] = (float)(ad * (double)w * 500.0 * (double)spg);
+  }
+}
+
 unsigned grid_for(int64_t n) {
   return (unsigned)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 16384);
 }
@@ -91,6 +121,52 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                      workspace, workspace_bytes, stream);
 }
 
+int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, float* grad_x, int64_t batch,
+                                     int64_t n_samples, int64_t ir_length, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (batch < 0 || n_samples < 1 || ir_length < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0) return DDSP_HIP_OK;
+  if (!grad || !spectrum || !grad_x) return DDSP_HIP_EINVAL;
+  return upols_apply(grad, batch, n_samples, spectrum, std::min(ir_length, n_samples), false, grad_x,
+                     workspace, workspace_bytes, stream, true);
+}
+
+size_t ddsp_hip_reverb_ir_grad_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length) {
+  if (batch < 1 || n_samples < 1 || ir_length < 1) return 0;
+  return upols_corr_workspace_bytes(batch, n_samples, ir_length);
+}
+
+int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impulse, int64_t batch,
+                            int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  if (batch < 0 || n_samples < 1 || ir_length < 1) return DDSP_HIP_EINVAL;
+  if (!grad_impulse) return DDSP_HIP_EINVAL;
+  const int64_t kc = std::min(ir_length, n_samples);
+  if (kc < ir_length) {  // taps past the input length were cropped: zero gradient
+    hipError_t e = hipMemsetAsync(grad_impulse + kc, 0, sizeof(float) * (ir_length - kc), S(stream));
+    if (e != hipSuccess) return DDSP_HIP_ELAUNCH;
+  }
+  if (batch == 0) {
+    hipError_t e = hipMemsetAsync(grad_impulse, 0, sizeof(float) * kc, S(stream));
+    return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;
+  }
+  if (!x || !grad) return DDSP_HIP_EINVAL;
+  return upols_corr(x, grad, batch, n_samples, ir_length, grad_impulse, workspace, workspace_bytes, stream);
+}
+
+int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
+                                     const float* grad_impulse, int64_t length, int64_t grad_length,
+                                     float sample_rate, float* grad_noise, float* grad_decay, float* grad_wet,
+                                     void* stream) {
+  if (length < 1 || grad_length < 0 || !noise || !decay || !wet || !grad_impulse || !grad_noise ||
+      !grad_decay || !grad_wet || !(sample_rate > 0))
+    return DDSP_HIP_EINVAL;
+  hipLaunchKernelGGL(impulse_backward_kernel, dim3(1), dim3(1024), 0, S(stream), noise, decay, wet,
+                     grad_impulse, std::min(grad_length, length), length, sample_rate, grad_noise,
+                     grad_decay, grad_wet);
+  return launch_status();
+}
+
 size_t ddsp_hip_fft_convolve_workspace_size(int64_t rows, int64_t kernel_rows, int64_t n) {
   if (rows < 1 || n < 1 || n <= kDirectMaxN) return 0;
   const bool per_row = kernel_rows != 1;
@@ -129,6 +205,6 @@ const char* ddsp_hip_status_string(int status) {
   }
 }
 
-int ddsp_hip_version(void) { return 101; }
+int ddsp_hip_version(void) { return 102; }
 
 }  // extern "C"

@@ -16,6 +16,14 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
                    void* stream);
 // y[rows, n] = (x[rows, n] (*) h)[0:n]; spectrum from upols_spectrum (one kernel shared by all
 // rows, or one per row when per_row_kernel).  klen = kernel length the spectrum was made with.
+// reverse: the transposed convolution y'[t] = sum_tau x[t+tau] h[tau] (input gradient), by
+// reading x and writing y time-reversed.
 int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
-                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream);
+                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream,
+                bool reverse = false);
+// dimp[tau] = sum_rows sum_t g[row][t+tau] x[row][t], tau < min(klen, n) (kernel gradient of a
+// kernel shared by all rows); writes min(klen, n) values.
+size_t upols_corr_workspace_bytes(int64_t rows, int64_t n, int64_t klen);
+int upols_corr(const float* x, const float* g, int64_t rows, int64_t n, int64_t klen, float* dimp, void* ws,
+               size_t ws_bytes, void* stream);
 }  // namespace ddsp

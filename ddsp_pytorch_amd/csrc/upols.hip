@@ -155,9 +155,13 @@ __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& 
   }
 }
 
-// X[pair][b][:] = FFT(z[(b-1)P, (b+1)P)); grid (nb, npairs)
+// X[pair][b][:] = FFT(z[(b+off)P, (b+off+2)P)); grid (nb, npairs).
+//   off = -1: the overlap-save input windows;  off = 0 with zero_hi: FFT([z_b, 0]) (the
+//   zero-padded blocks of the IR-gradient correlation);  reverse: z read time-reversed
+//   (z'[s] = z[T-1-s], the transposed convolution of the input gradient).
 __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
                                                             int64_t T, int rows, int pairing, int nb,
+                                                            int off, int zero_hi, int reverse,
                                                             float2* __restrict__ X) {
   __shared__ float2 lds[kPad];
   const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
@@ -165,13 +169,14 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
   pair_rows(pair, rows, pairing, ra, rb);
   const float* xa = x + (int64_t)ra * ld;
   const float* xb = rb >= 0 ? x + (int64_t)rb * ld : nullptr;
-  const int64_t s0 = (int64_t)(b - 1) * kP;
+  const int64_t s0 = (int64_t)(b + off) * kP;
   float2 v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t s = s0 + j + 256 * r;
-    const bool ok = s >= 0 && s < T;
-    v[r] = make_float2(ok ? xa[s] : 0.0f, (ok && xb) ? xb[s] : 0.0f);
+    const bool ok = s >= 0 && s < T && !(zero_hi && r >= 8);
+    const int64_t si = reverse ? T - 1 - s : s;
+    v[r] = make_float2(ok ? xa[si] : 0.0f, (ok && xb) ? xb[si] : 0.0f);
   }
   fft4096<false>(v, lds);
   float2* out = X + ((int64_t)pair * nb + b) * kN;
@@ -246,7 +251,7 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
 
 // y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
 __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __restrict__ Y, int nb,
-                                                            int64_t T, int rows, int pairing,
+                                                            int64_t T, int rows, int pairing, int reverse,
                                                             float* __restrict__ y, int64_t ld) {
   __shared__ float2 lds[kPad];
   const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
@@ -263,9 +268,80 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
   for (int r = 8; r < 16; ++r) {
     const int64_t s = (int64_t)b * kP + j + 256 * r - kP;
     if (s < T) {
-      ya[s] = v[r].x;
-      if (yb) yb[s] = v[r].y;
+      const int64_t so = reverse ? T - 1 - s : s;
+      ya[so] = v[r].x;
+      if (yb) yb[so] = v[r].y;
     }
+  }
+}
+
+// IR-gradient correlation (backward of Reverb.forward w.r.t. the impulse, modules.py:28-35):
+//   dH_p[f] = sum_{pair in group} sum_j conj(Xz[pair][j][f]) * Gw[pair][j+p][f]
+// with Xz_j = FFT([x_j, 0]) and Gw_k = FFT([g_k, g_{k+1}]): the circular correlation of the two
+// 2P windows is the exact linear correlation for lags pP + [0, P).  For a packed pair
+// (z = x_a + i x_b, same for g) the real part of the inverse transform is corr_a + corr_b, so
+// the packed spectra are used as they are.  One bin per thread, PC consecutive partitions with
+// a sliding register window of conj(Xz); grid (N/256, ceil(Q/PC), groups).
+template <int PC>
+__global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restrict__ Xz,
+                                                         const float2* __restrict__ Gw, int nb, int Q,
+                                                         int npairs, int pairs_per_group,
+                                                         float2* __restrict__ part) {
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int p0 = blockIdx.y * PC;
+  const int grp = blockIdx.z;
+  const float2 zero = make_float2(0.f, 0.f);
+  float2 acc[PC];
+#pragma unroll
+  for (int d = 0; d < PC; ++d) acc[d] = zero;
+  const int pr0 = grp * pairs_per_group, pr1 = min(npairs, pr0 + pairs_per_group);
+  for (int pair = pr0; pair < pr1; ++pair) {
+    const float2* Xp = Xz + (int64_t)pair * nb * kN + f;
+    const float2* Gp = Gw + (int64_t)pair * nb * kN + f;
+    float2 win[PC];
+#pragma unroll
+    for (int d = 0; d < PC; ++d) win[d] = zero;
+    for (int k = p0; k < nb; ++k) {
+#pragma unroll
+      for (int d = PC - 1; d > 0; --d) win[d] = win[d - 1];
+      const float2 xv = Xp[(int64_t)(k - p0) * kN];
+      win[0] = make_float2(xv.x, -xv.y);
+      const float2 g = Gp[(int64_t)k * kN];
+#pragma unroll
+      for (int d = 0; d < PC; ++d) {
+        acc[d].x = fmaf(win[d].x, g.x, fmaf(-win[d].y, g.y, acc[d].x));
+        acc[d].y = fmaf(win[d].x, g.y, fmaf(win[d].y, g.x, acc[d].y));
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < PC; ++d)
+    if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = acc[d];
+}
+
+// dimp[pP + n] = Re(IFFT(sum_groups part[grp][p])) [n] / N for n < P, pP + n < klen; grid (Q)
+__global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __restrict__ part, int groups,
+                                                                int Q, int64_t klen, float* __restrict__ dimp) {
+  __shared__ float2 lds[kPad];
+  const int p = blockIdx.x, j = threadIdx.x;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = make_float2(0.f, 0.f);
+  for (int g = 0; g < groups; ++g) {
+    const float2* in = part + ((int64_t)g * Q + p) * kN;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float2 w = in[j + 256 * r];
+      v[r].x += w.x;
+      v[r].y += w.y;
+    }
+  }
+  fft4096<true>(v, lds);
+  const float inv_n = 1.0f / (float)kN;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int64_t s = (int64_t)p * kP + j + 256 * r;
+    if (s < klen) dimp[s] = v[r].x * inv_n;
   }
 }
 
@@ -295,7 +371,7 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
 }
 
 int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
-                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream) {
+                bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream, bool reverse) {
   const bool pairing = !per_row_kernel;
   const int64_t npairs = pairing ? (rows + 1) / 2 : rows;
   const int64_t nb = upols_blocks(n);
@@ -305,7 +381,7 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
   hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     x, n, n, (int)rows, (int)pairing, (int)nb, X);
+                     x, n, n, (int)rows, (int)pairing, (int)nb, -1, 0, (int)reverse, X);
   int st = launch_status();
   if (st) return st;
   const int64_t h_stride = per_row_kernel ? upols_partitions(klen) * kN : 0;
@@ -316,7 +392,43 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
                      (int)nb, (int)Q, Y);
   if ((st = launch_status())) return st;
   hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     Y, (int)nb, n, (int)rows, (int)pairing, y, n);
+                     Y, (int)nb, n, (int)rows, (int)pairing, (int)reverse, y, n);
+  return launch_status();
+}
+
+size_t upols_corr_workspace_bytes(int64_t rows, int64_t n, int64_t klen) {
+  const int64_t npairs = (rows + 1) / 2;
+  const int64_t nb = upols_blocks(n);
+  const int64_t Q = upols_partitions(std::min(klen, n));
+  const int64_t groups = std::min<int64_t>(npairs, 16);
+  return (2 * (size_t)npairs * nb + (size_t)groups * Q) * kN * sizeof(float2);
+}
+
+int upols_corr(const float* x, const float* g, int64_t rows, int64_t n, int64_t klen, float* dimp, void* ws,
+               size_t ws_bytes, void* stream) {
+  const int64_t npairs = (rows + 1) / 2;
+  const int64_t nb = upols_blocks(n);
+  const int64_t kc = std::min(klen, n);
+  const int64_t Q = upols_partitions(kc);
+  const int64_t groups = std::min<int64_t>(npairs, 16);
+  const int64_t ppg = (npairs + groups - 1) / groups;
+  if (!ws || ws_bytes < upols_corr_workspace_bytes(rows, n, klen)) return DDSP_HIP_EWORKSPACE;
+  if (nb > INT32_MAX || npairs > 65535 || Q > 65535) return DDSP_HIP_EINVAL;
+  float2* Xz = reinterpret_cast<float2*>(ws);
+  float2* Gw = Xz + (size_t)npairs * nb * kN;
+  float2* part = Gw + (size_t)npairs * nb * kN;
+  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
+                     x, n, n, (int)rows, 1, (int)nb, 0, 1, 0, Xz);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
+                     g, n, n, (int)rows, 1, (int)nb, 0, 0, 0, Gw);
+  if ((st = launch_status())) return st;
+  hipLaunchKernelGGL(upols_corr_kernel<16>, dim3(kN / kNT, (unsigned)((Q + 15) / 16), (unsigned)groups),
+                     dim3(kNT), 0, S(stream), Xz, Gw, (int)nb, (int)Q, (int)npairs, (int)ppg, part);
+  if ((st = launch_status())) return st;
+  hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Q), dim3(kNT), 0, S(stream), part, (int)groups,
+                     (int)Q, kc, dimp);
   return launch_status();
 }
 

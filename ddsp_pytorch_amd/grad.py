@@ -1,0 +1,377 @@
+"""Autograd for the gfx950 synthesis path (training).
+
+The reference trains by back-propagating a multiscale spectral loss through
+``DDSPDecoder.forward`` (train.py:84-130).  Every differentiable entry point of
+``core.py`` dispatches here when autograd needs it; each ``torch.autograd.Function``
+runs the forward kernel and, in ``backward``, the matching vector-Jacobian kernel of
+``csrc/backward.hip`` / ``csrc/upols.hip`` through the C-ABI (include/ddsp_hip.h).
+
+Pitch (f0) is an input feature in the reference's training loop (``batch['pitch']``,
+train.py:84-99): no gradient flows to it.  ``remove_above_nyquist`` gives f0 the zero
+gradient the reference's comparison gives; the oscillator ops refuse an f0 that
+requires grad rather than silently returning a wrong (zero) gradient.
+"""
+import torch
+
+from . import _lib
+from . import core
+
+_F = torch.autograd.Function
+
+
+def _g(t):
+    """contiguous, 16-byte aligned upstream gradient."""
+    return core._c(t)
+
+
+def refuse_f0_grad(f0, name):
+    if torch.is_grad_enabled() and f0.requires_grad:
+        raise NotImplementedError(
+            f"ddsp_hip {name}: no gradient w.r.t. f0 (pitch is an input feature in the reference's "
+            "training loop, train.py:84-99); pass f0.detach()")
+
+
+def wants_grad(*tensors):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
+# ------------------------------------------------------------------------------------------
+class ScaleFn(_F):
+    """core.py:77-78 (+ the bias of modules.py:113)."""
+
+    @staticmethod
+    def forward(ctx, x, bias):
+        ctx.save_for_backward(x)
+        ctx.bias = float(bias)
+        return core.scale_with_bias(x, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        x, g = core._c(x), _g(g)
+        dx = torch.empty_like(x)
+        _lib.call("scale_function_backward", _lib.ptr(x), _lib.ptr(g), _lib.ptr(dx), x.numel(), ctx.bias,
+                  _lib.stream_of(x))
+        return dx, None
+
+
+class NyquistFn(_F):
+    """core.py:70-74: d amplitudes = grad * mask; f0 enters only through a comparison (zero grad)."""
+
+    @staticmethod
+    def forward(ctx, amplitudes, f0, sample_rate):
+        ctx.save_for_backward(f0)
+        ctx.sr = sample_rate
+        ctx.shape = amplitudes.shape
+        return core.remove_above_nyquist(amplitudes, f0, sample_rate)
+
+    @staticmethod
+    def backward(ctx, g):
+        (f0,) = ctx.saved_tensors
+        d = core.remove_above_nyquist(g, f0.detach(), ctx.sr)
+        if d.shape != ctx.shape:
+            d = d.sum_to_size(ctx.shape)
+        return d, None, None
+
+
+class UpsampleFn(_F):
+    """core.py:64-67: nearest upsampling; backward sums each block."""
+
+    @staticmethod
+    def forward(ctx, signal, factor):
+        ctx.shape = signal.shape
+        ctx.factor = int(factor)
+        return core.upsample(signal, factor)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, F, C = ctx.shape
+        g = _g(g)
+        d = torch.empty(B, F, C, dtype=torch.float32, device=g.device)
+        _lib.call("upsample_backward", _lib.ptr(g), _lib.ptr(d), B, F, C, ctx.factor, _lib.stream_of(g))
+        return d, None
+
+
+class HarmonicSynthFn(_F):
+    """core.py:136-141 at the op boundary: d amplitudes[b,t,k] = g[b,t] sin(fl32(w[b,t] k))."""
+
+    @staticmethod
+    def forward(ctx, f0, amplitudes, sample_rate):
+        ctx.save_for_backward(f0)
+        ctx.sr = sample_rate
+        ctx.H = amplitudes.shape[-1]
+        return core.harmonic_synth(f0, amplitudes, sample_rate)
+
+    @staticmethod
+    def backward(ctx, g):
+        (f0,) = ctx.saved_tensors
+        B, T = f0.shape[0], f0.shape[1]
+        omega = core.phase(f0.detach(), ctx.sr)
+        g = _g(g)
+        dA = torch.empty(B, T, ctx.H, dtype=torch.float32, device=g.device)
+        _lib.call("harmonic_synth_backward", _lib.ptr(omega), _lib.ptr(g), _lib.ptr(dA), B, T, ctx.H,
+                  _lib.stream_of(g))
+        return None, dA, None
+
+
+class ImpulseResponseFn(_F):
+    """core.py:144-166: the transposed filter design (a cosine transform of the windowed taps)."""
+
+    @staticmethod
+    def forward(ctx, amp, target_size):
+        ctx.shape = amp.shape
+        ctx.target = int(target_size)
+        return core.amp_to_impulse_response(amp, target_size)
+
+    @staticmethod
+    def backward(ctx, g):
+        NB = ctx.shape[-1]
+        g = _g(g)
+        rows = g.numel() // ctx.target
+        d = torch.empty(ctx.shape, dtype=torch.float32, device=g.device)
+        _lib.call("amp_to_impulse_response_backward", _lib.ptr(g), _lib.ptr(d), rows, NB, ctx.target,
+                  _lib.stream_of(g))
+        return d, None
+
+
+class FFTConvolveFn(_F):
+    """core.py:169-176: y = (s (*) k)[:N].  Both gradients are correlations with g:
+    d s = flip((flip g) (*) k), d k = flip((flip g) (*) s), each on the same convolution kernels."""
+
+    @staticmethod
+    def forward(ctx, signal, kernel):
+        ctx.save_for_backward(signal, kernel)
+        return core.fft_convolve(signal, kernel)
+
+    @staticmethod
+    def backward(ctx, g):
+        s, k = ctx.saved_tensors
+        gr = torch.flip(g, (-1,))
+        ds = dk = None
+        if ctx.needs_input_grad[0]:
+            ds = torch.flip(core.fft_convolve(gr, k.detach()), (-1,)).sum_to_size(s.shape)
+        if ctx.needs_input_grad[1]:
+            dk = torch.flip(core.fft_convolve(gr, s.detach()), (-1,)).sum_to_size(k.shape)
+        return ds, dk
+
+
+# ------------------------------------------------------------------------------------------
+class ControlsFn(_F):
+    """modules.py:44-67 HarmonicSynth.get_controls."""
+
+    @staticmethod
+    def forward(ctx, amplitudes, distribution, f0, sample_rate):
+        ctx.save_for_backward(amplitudes, distribution, f0)
+        ctx.sr = sample_rate
+        return core.harmonic_controls(amplitudes, distribution, f0, sample_rate)
+
+    @staticmethod
+    def backward(ctx, g_amp, g_dist):
+        a, d, f0 = ctx.saved_tensors
+        B, F, H = d.shape
+        a_v, a_ld = core._rows_view(a, "amplitudes")
+        d_v, d_ld = core._rows_view(d, "harmonic_distribution")
+        g_amp = _g(g_amp) if g_amp is not None else torch.zeros(B, F, 1, device=d.device)
+        g_dist = _g(g_dist) if g_dist is not None else torch.zeros(B, F, H, device=d.device)
+        da = torch.empty(B, F, 1, dtype=torch.float32, device=d.device)
+        dd = torch.empty(B, F, H, dtype=torch.float32, device=d.device)
+        _lib.call("harmonic_controls_backward", _lib.ptr(a_v), a_ld, _lib.ptr(d_v), d_ld, _lib.ptr(core._c(f0)),
+                  _lib.ptr(g_amp), _lib.ptr(g_dist), _lib.ptr(da), _lib.ptr(dd), B * F, H, float(ctx.sr),
+                  _lib.stream_of(dd))
+        return da, dd, None, None
+
+
+class SynthFramesHarmonicFn(_F):
+    """modules.py:69-80 HarmonicSynth.forward (frame-rate controls in, audio out)."""
+
+    @staticmethod
+    def forward(ctx, f0, amplitudes, distribution, block_size, sample_rate):
+        ctx.f0 = f0.detach()
+        ctx.amp = core._c(amplitudes.detach())
+        # the caller multiplies `distribution` in place afterwards (modules.py:73): keep its
+        # pre-multiplication value for the amplitude gradient
+        ctx.dist = core._c(distribution.detach()).clone()
+        ctx.bs, ctx.sr = int(block_size), float(sample_rate)
+        return core.harmonic_synth_frames(f0, amplitudes, distribution, block_size, sample_rate,
+                                          write_back=False)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, F, H = ctx.dist.shape
+        g = _g(g)
+        da = torch.empty(B, F, 1, dtype=torch.float32, device=g.device)
+        dd = torch.empty(B, F, H, dtype=torch.float32, device=g.device)
+        _lib.call("harmonic_synth_frames_backward", _lib.ptr(core._c(ctx.f0)), _lib.ptr(ctx.amp),
+                  _lib.ptr(ctx.dist), _lib.ptr(g), _lib.ptr(da), _lib.ptr(dd), B, F, H, ctx.bs, ctx.sr,
+                  _lib.stream_of(g))
+        return None, da, dd, None, None
+
+
+def params_backward(f0, param, g, block_size, sample_rate):
+    B, F, H1 = param.shape
+    dp = torch.empty(B, F, H1, dtype=torch.float32, device=param.device)
+    _lib.call("harmonic_synth_params_backward", _lib.ptr(core._c(f0)), _lib.ptr(core._c(param)), _lib.ptr(g),
+              _lib.ptr(dp), B, F, H1 - 1, int(block_size), float(sample_rate), _lib.stream_of(dp))
+    return dp
+
+
+def noise_backward(mags, noise, seed, offset, raw_bias, g, block_size):
+    B, F, NB = mags.shape
+    dm = torch.empty(B, F, NB, dtype=torch.float32, device=mags.device)
+    raw = raw_bias is not None
+    _lib.call("filtered_noise_backward", _lib.ptr(core._c(mags) if raw else None), _lib.ptr(noise), seed, offset,
+              int(raw), float(raw_bias if raw else 0.0), _lib.ptr(g), _lib.ptr(dm), B, F, NB, int(block_size),
+              _lib.stream_of(dm))
+    return dm
+
+
+class HarmonicParamsFn(_F):
+    """decoder.py:106-113 + modules.py:44-80 from the raw harmonic projection."""
+
+    @staticmethod
+    def forward(ctx, f0, param, block_size, sample_rate):
+        ctx.save_for_backward(f0, param)
+        ctx.bs, ctx.sr = int(block_size), float(sample_rate)
+        return core.harmonic_synth_params(f0, param, block_size, sample_rate)
+
+    @staticmethod
+    def backward(ctx, g):
+        f0, param = ctx.saved_tensors
+        return None, params_backward(f0.detach(), param.detach(), _g(g), ctx.bs, ctx.sr), None, None
+
+
+class FilteredNoiseFn(_F):
+    """modules.py:111-128 (raw_bias given: get_controls fused).  The forward's noise — injected, or
+    the Philox (seed, offset) it drew on the device — is what the backward correlates with."""
+
+    @staticmethod
+    def forward(ctx, magnitudes, add, block_size, noise, raw_bias, return_noise):
+        seed, offset = core._noise_counter.next() if noise is None else (0, 0)
+        outs = core._filtered_noise_launch(magnitudes, block_size, noise, add, return_noise, raw_bias, seed,
+                                           offset)
+        ctx.mags = magnitudes.detach()
+        ctx.noise = noise
+        ctx.seed, ctx.offset = seed, offset
+        ctx.raw_bias = raw_bias
+        ctx.bs = int(block_size)
+        ctx.two = isinstance(outs, tuple)
+        return outs
+
+    @staticmethod
+    def backward(ctx, g_out, g_nout=None):
+        g = g_out if (g_nout is None) else (g_nout if g_out is None else g_out + g_nout)
+        g_f = _g(g)
+        dm = noise_backward(ctx.mags, ctx.noise, ctx.seed, ctx.offset, ctx.raw_bias, g_f, ctx.bs)
+        d_add = g_out if ctx.needs_input_grad[1] else None
+        return dm, d_add, None, None, None, None
+
+
+class SynthFramesFn(_F):
+    """decoder.py:106-121 in one kernel; backward = harmonic params + raw noise VJPs."""
+
+    @staticmethod
+    def forward(ctx, f0, param, mags, block_size, sample_rate, bias, noise, parts):
+        seed, offset = core._noise_counter.next() if noise is None else (0, 0)
+        outs = core._synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, parts, seed,
+                                         offset)
+        ctx.save_for_backward(f0, param, mags)
+        ctx.noise, ctx.seed, ctx.offset = noise, seed, offset
+        ctx.bs, ctx.sr, ctx.bias = int(block_size), float(sample_rate), float(bias)
+        return outs
+
+    @staticmethod
+    def backward(ctx, g_out, g_harm=None, g_nz=None):
+        f0, param, mags = ctx.saved_tensors
+        gh = g_out if g_harm is None else g_out + g_harm
+        gn = g_out if g_nz is None else g_out + g_nz
+        dp = dm = None
+        if ctx.needs_input_grad[1]:
+            dp = params_backward(f0.detach(), param.detach(), _g(gh), ctx.bs, ctx.sr)
+        if ctx.needs_input_grad[2]:
+            dm = noise_backward(mags.detach(), ctx.noise, ctx.seed, ctx.offset, ctx.bias, _g(gn), ctx.bs)
+        return None, dp, dm, None, None, None, None, None
+
+
+# ------------------------------------------------------------------------------------------
+def reverb_transposed(g, spectrum, ir_length):
+    B, T = g.shape[0], g.shape[1]
+    dx = torch.empty(B, T, 1, dtype=torch.float32, device=g.device)
+    ws = core._workspace(_lib.query("reverb_workspace_size", B, T, int(ir_length)), g.device)
+    _lib.call("reverb_apply_transposed", _lib.ptr(g), _lib.ptr(spectrum), _lib.ptr(dx), B, T, int(ir_length),
+              _lib.ptr(ws), ws.numel(), _lib.stream_of(g))
+    return dx
+
+
+def reverb_ir_grad(x, g, ir_length):
+    B, T = x.shape[0], x.shape[1]
+    dimp = torch.empty(int(ir_length), dtype=torch.float32, device=x.device)
+    ws = core._workspace(_lib.query("reverb_ir_grad_workspace_size", B, T, int(ir_length)), x.device)
+    _lib.call("reverb_ir_grad", _lib.ptr(x), _lib.ptr(g), _lib.ptr(dimp), B, T, int(ir_length), _lib.ptr(ws),
+              ws.numel(), _lib.stream_of(x))
+    return dimp
+
+
+def impulse_backward(noise, decay, wet, dimp, grad_length, sample_rate):
+    L = noise.shape[0]
+    dn = torch.empty_like(core._c(noise))
+    dd = torch.empty((), dtype=torch.float32, device=noise.device)
+    dw = torch.empty((), dtype=torch.float32, device=noise.device)
+    _lib.call("reverb_impulse_backward", _lib.ptr(core._c(noise)), _lib.ptr(core._c(decay)), _lib.ptr(core._c(wet)),
+              _lib.ptr(dimp), L, int(grad_length), float(sample_rate), _lib.ptr(dn), _lib.ptr(dd), _lib.ptr(dw),
+              _lib.stream_of(dn))
+    return dn.reshape(noise.shape), dd.reshape(decay.shape), dw.reshape(wet.shape)
+
+
+class ReverbApplyFn(_F):
+    """modules.py:28-35 with a fixed (cached) IR spectrum: gradient w.r.t. the signal only."""
+
+    @staticmethod
+    def forward(ctx, x, spectrum, ir_length):
+        ctx.spectrum = spectrum
+        ctx.L = int(ir_length)
+        return core.reverb_apply(x, spectrum, ir_length)
+
+    @staticmethod
+    def backward(ctx, g):
+        return reverb_transposed(_g(g), ctx.spectrum, ctx.L), None, None
+
+
+class ReverbFn(_F):
+    """modules.py:21-35 Reverb.build_impulse + forward: gradients for the signal and for the
+    reverb's parameters (noise, decay, wet)."""
+
+    @staticmethod
+    def forward(ctx, x, noise, decay, wet, spectrum, ir_length, sample_rate):
+        ctx.save_for_backward(x, noise, decay, wet)
+        ctx.spectrum = spectrum
+        ctx.L, ctx.sr = int(ir_length), float(sample_rate)
+        return core.reverb_apply(x, spectrum, ir_length)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, noise, decay, wet = ctx.saved_tensors
+        g = _g(g)
+        dx = reverb_transposed(g, ctx.spectrum, ctx.L) if ctx.needs_input_grad[0] else None
+        dn = dd = dw = None
+        if any(ctx.needs_input_grad[1:4]):
+            T = x.shape[1]
+            dimp = reverb_ir_grad(core._c(x.detach()), g, ctx.L)
+            dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), dimp, min(ctx.L, T), ctx.sr)
+        return dx, dn, dd, dw, None, None, None
+
+
+class BuildImpulseFn(_F):
+    """modules.py:21-26 Reverb.build_impulse."""
+
+    @staticmethod
+    def forward(ctx, noise, decay, wet, sample_rate):
+        ctx.save_for_backward(noise, decay, wet)
+        ctx.sr = float(sample_rate)
+        return core.reverb_build_impulse(noise, decay, wet, sample_rate)
+
+    @staticmethod
+    def backward(ctx, g):
+        noise, decay, wet = ctx.saved_tensors
+        g = _g(g).reshape(-1)
+        dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), g, noise.shape[0], ctx.sr)
+        return dn, dd, dw, None

@@ -14,7 +14,7 @@ kernel (throughput mode: no host RNG, no H2D copy, no HBM read of noise).
 import torch
 import torch.nn as nn
 
-from . import core
+from . import core, grad
 
 NOISE_MODES = ("torch", "device")
 
@@ -49,8 +49,12 @@ class Reverb(nn.Module):
         return self._spec
 
     def forward(self, x):
-        """modules.py:28-35: IR padded/cropped to len(x), causal convolution truncated to len(x)."""
-        return core.reverb_apply(x, Reverb._spectrum(self, x.shape[1]), self.length)
+        """modules.py:28-35: IR padded/cropped to len(x), causal convolution truncated to len(x).
+        Under autograd the signal and the reverb parameters (noise, decay, wet) get gradients."""
+        spec = Reverb._spectrum(self, x.shape[1])
+        if core._wants_grad(x, self.noise, self.decay, self.wet):
+            return grad.ReverbFn.apply(x, self.noise, self.decay, self.wet, spec, self.length, self.sample_rate)
+        return core.reverb_apply(x, spec, self.length)
 
 
 class HarmonicSynth(nn.Module):

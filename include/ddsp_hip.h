@@ -159,6 +159,82 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* ---------------- backward (training): train.py:84-130 back-propagates through the path ----------------
+ * Vector-Jacobian products of the entry points above.  `grad*` inputs are the upstream
+ * gradients (same shapes as the forward outputs), `grad_*` outputs are caller-allocated and
+ * overwritten.  Pitch (f0) is an input feature in the reference's training loop and gets no
+ * gradient. */
+
+/* core.py:77-78 scale_function backward: dx = grad * scale'(x + bias). */
+int ddsp_hip_scale_function_backward(const float* x, const float* grad, float* dx, int64_t n, float bias,
+                                     void* stream);
+
+/* core.py:64-67 upsample backward: dx[B,F,C] = sum over each block of grad[B,F*factor,C]. */
+int ddsp_hip_upsample_backward(const float* grad, float* dx, int64_t batch, int64_t frames, int64_t channels,
+                               int64_t factor, void* stream);
+
+/* core.py:136-141 harmonic_synth backward w.r.t. amplitudes at the op boundary:
+ * grad_amplitudes[B,T,H] = grad[B,T] * sin(fl32(omega[B,T] * k)); omega from ddsp_hip_phase. */
+int ddsp_hip_harmonic_synth_backward(const float* omega, const float* grad, float* grad_amplitudes,
+                                     int64_t batch, int64_t n_samples, int64_t n_harmonic, void* stream);
+
+/* core.py:144-166 amp_to_impulse_response backward: grad_impulse[rows,target] -> grad_amp[rows,NB]. */
+int ddsp_hip_amp_to_impulse_response_backward(const float* grad_impulse, float* grad_amp, int64_t rows,
+                                              int64_t n_bands, int64_t target_size, void* stream);
+
+/* modules.py:44-67 HarmonicSynth.get_controls backward: (grad_amplitudes[rows], grad_distribution
+ * [rows,H]) -> gradients of the raw inputs (strided as in ddsp_hip_harmonic_controls). */
+int ddsp_hip_harmonic_controls_backward(const float* amplitudes_raw, int64_t amp_stride,
+                                        const float* distribution_raw, int64_t dist_stride, const float* f0,
+                                        const float* grad_amplitudes, const float* grad_distribution,
+                                        float* grad_amplitudes_raw, float* grad_distribution_raw,
+                                        int64_t rows, int64_t n_harmonic, float sample_rate, void* stream);
+
+/* modules.py:69-80 HarmonicSynth.forward backward (ddsp_hip_harmonic_synth_frames): the sine products
+ * summed over each block, dA[b,f,k] = sum_t grad[t] sin(w_t k), then grad_distribution = dA * amp and
+ * grad_amplitudes = sum_k dA * distribution.  `distribution` is the normalised distribution
+ * BEFORE the in-place multiplication by the amplitudes. */
+int ddsp_hip_harmonic_synth_frames_backward(const float* f0, const float* amplitudes, const float* distribution,
+                                            const float* grad, float* grad_amplitudes,
+                                            float* grad_distribution, int64_t batch, int64_t frames,
+                                            int64_t n_harmonic, int64_t block_size, float sample_rate,
+                                            void* stream);
+
+/* decoder.py:106-113 + modules.py:44-80 backward (ddsp_hip_harmonic_synth_params, and the harmonic
+ * half of ddsp_hip_synth_frames): grad[B,F*bs] -> grad_param[B,F,H+1]. */
+int ddsp_hip_harmonic_synth_params_backward(const float* f0, const float* param, const float* grad,
+                                            float* grad_param, int64_t batch, int64_t frames,
+                                            int64_t n_harmonic, int64_t block_size, float sample_rate,
+                                            void* stream);
+
+/* modules.py:111-128 FilteredNoise backward (ddsp_hip_filtered_noise[_params], the noise half of
+ * ddsp_hip_synth_frames): grad[B,F*bs] -> grad_magnitudes[B,F,NB].  The noise is `noise` as given
+ * to the forward, or (noise == NULL) regenerated from the forward's (seed, offset).  raw != 0:
+ * `magnitudes` are the raw projections and scale_function(x + bias) is differentiated too. */
+int ddsp_hip_filtered_noise_backward(const float* magnitudes, const float* noise, uint64_t seed, uint64_t offset,
+                                     int raw, float bias, const float* grad, float* grad_magnitudes,
+                                     int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
+                                     void* stream);
+
+/* modules.py:28-35 Reverb.forward backward.
+ *   ddsp_hip_reverb_apply_transposed: grad_x[b,t] = sum_tau grad[b,t+tau] IR[tau] (same spectrum and
+ *     workspace as ddsp_hip_reverb_apply);
+ *   ddsp_hip_reverb_ir_grad: grad_impulse[tau] = sum_b sum_t grad[b,t+tau] x[b,t] for tau < L
+ *     (zero for taps cropped away when L > n_samples);
+ *   ddsp_hip_reverb_impulse_backward (modules.py:21-26): grad_impulse -> grad_noise[L], and the
+ *     device scalars grad_decay, grad_wet (taps >= grad_length carry no gradient). */
+int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, float* grad_x, int64_t batch,
+                                     int64_t n_samples, int64_t ir_length, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+size_t ddsp_hip_reverb_ir_grad_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length);
+int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impulse, int64_t batch,
+                            int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
+                            void* stream);
+int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
+                                     const float* grad_impulse, int64_t length, int64_t grad_length,
+                                     float sample_rate, float* grad_noise, float* grad_decay, float* grad_wet,
+                                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,9 +98,9 @@ def noise_forward(magnitudes, noise, block_size):
     return y.reshape(y.shape[0], -1, 1)
 
 
-@torch.no_grad()
-def synth_path(f0, param, mags, noise, reverb, block_size, sample_rate):
-    """Frame-rate controls -> audio: the synthesis section of ddsp/models/decoder.py:106-125."""
+def synth_path_autograd(f0, param, mags, noise, reverb, block_size, sample_rate):
+    """Frame-rate controls -> audio: the synthesis section of ddsp/models/decoder.py:106-125,
+    differentiable (the gradient checker for the backward kernels)."""
     amp, dist = harmonic_controls(param[..., :1], param[..., 1:], f0, sample_rate)
     harmonic = harmonic_forward(amp, dist, f0, block_size, sample_rate)
     mags = scale_function(mags + (-5.0))
@@ -109,3 +109,7 @@ def synth_path(f0, param, mags, noise, reverb, block_size, sample_rate):
     if reverb is not None:
         signal = reverb(signal)
     return signal
+
+
+synth_path = torch.no_grad()(synth_path_autograd)
+synth_path.__doc__ = "synth_path_autograd under torch.no_grad() (the CPU baseline's forward)."

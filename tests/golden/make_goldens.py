@@ -191,6 +191,49 @@ def main():
          distribution=o["harmonic_ctrls"]["harmonic_distribution"],
          magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
 
+    grad_goldens(decoder, modules, sr)
+
+
+@torch.enable_grad()
+def grad_goldens(decoder, modules, sr):
+    # ---------------- g6: gradients (train.py:84-130 back-propagates through the path) ----------------
+    # loss = sum(signal * w) with a fixed random w, so d loss / d signal = w exactly.
+    torch.manual_seed(0)
+    model = decoder.DDSPDecoder(32, 100, 65, sr, 512, True)
+    acts = {}
+
+    def keep(name):
+        def hook(mod, inp, out):
+            out.retain_grad()
+            acts[name] = out
+        return hook
+
+    model.harmonic_proj.register_forward_hook(keep("param"))
+    model.noise_proj.register_forward_hook(keep("mags"))
+    f0, loudness, _, _ = synth_inputs(4, 1, 16, 100, 65)
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness})
+    w = torch.randn(o["signal"].shape, generator=torch.Generator().manual_seed(15))
+    (o["signal"] * w).sum().backward()
+    grads = {"grad." + k: v.grad for k, v in model.named_parameters() if v.grad is not None}
+    sd = {"sd." + k: v for k, v in model.state_dict().items()}
+    save("g6_grad_decoder", hidden_size=32, n_harmonic=100, n_bands=65, sample_rate=sr, block_size=512,
+         pitch=f0, loudness=loudness, weight=w, signal=o["signal"].detach(),
+         param=acts["param"].detach(), mags=acts["mags"].detach(),
+         grad_param=acts["param"].grad, grad_mags=acts["mags"].grad, **grads, **sd)
+    # reverb alone, incl. the crop case (L > T)
+    for tag, L, T, B in (("small", 4800, 9600, 3), ("crop", 48000, 24000, 1)):
+        torch.manual_seed(1)
+        rv = modules.Reverb(L, sr, initial_wet=0.5, initial_decay=3.0)
+        g = torch.Generator().manual_seed(16)
+        x = (torch.randn(B, T, 1, generator=g) * 0.3).requires_grad_(True)
+        out = rv(x)
+        w = torch.randn(out.shape, generator=g)
+        (out * w).sum().backward()
+        save(f"g6_grad_reverb_{tag}", length=L, sample_rate=sr, noise=rv.noise.detach(), decay=rv.decay.detach(),
+             wet=rv.wet.detach(), x=x.detach(), weight=w, out=out.detach(), grad_x=x.grad,
+             grad_noise=rv.noise.grad, grad_decay=rv.decay.grad, grad_wet=rv.wet.grad)
+
 
 if __name__ == "__main__":
     main()
