@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-gather", action="store_true",
                    help="N>1: skip the synth + RCCL gather-to-rank-0 leg (reported separately as "
                         "'gathered'; value is always the left-sharded throughput)")
+    p.add_argument("--no-train-leg", action="store_true",
+                   help="skip the training-step leg (synthesis forward + backward kernels)")
     p.add_argument("--no-decoder-leg", action="store_true",
                    help="skip the full DDSPDecoder.forward leg (GRU/MLP + synthesis)")
     p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
@@ -146,6 +148,51 @@ def cpu_baseline(args, rank_inputs_seed=0):
                       f"config {args.config} (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
                       f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {len(times)} runs, "
                       f"{t:.3f} s each"}
+
+
+def train_leg(args, inp, dev, reps=20):
+    """one training step of the synthesis path — forward (synth_frames +
+    reverb) and backward (reverb input/IR gradients, harmonic and noise VJPs) for an upstream
+    gradient w, i.e. what train.py:84-130 runs below the decoder network."""
+    from ddsp_pytorch_amd import core
+    from ddsp_pytorch_amd.modules import Reverb
+    B, F, H, NB, bs, sr = (args.batch, args.frames, args.harmonics, args.bands, args.block_size,
+                           args.sample_rate)
+    torch.manual_seed(1)
+    rv = Reverb(args.reverb_length, sr).to(dev)
+    param = inp["param"].clone().requires_grad_(True)
+    mags = inp["mags"].clone().requires_grad_(True)
+    w = torch.randn(B, F * bs, 1, device=dev)
+    ev = {k: [] for k in ("forward", "backward")}
+
+    def step(timed):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        param.grad = mags.grad = None
+        for p_ in rv.parameters():
+            p_.grad = None
+        e[0].record()
+        sig = core.synth_frames(inp["f0"], param, mags, bs, sr)
+        out = rv(sig)
+        e[1].record()
+        out.backward(w)
+        e[2].record()
+        if timed:
+            ev["forward"].append((e[0], e[1]))
+            ev["backward"].append((e[1], e[2]))
+
+    for _ in range(3):
+        step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step(True)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    assert torch.isfinite(param.grad).all() and torch.isfinite(mags.grad).all()
+    ms = {k: round(sum(a.elapsed_time(b) for a, b in v) / len(v), 4) for k, v in ev.items()}
+    return {"value": round(B * F * bs / t, 1), "unit": "samples/s", "ms_per_step": round(t * 1e3, 4),
+            "event_ms": ms, "gradients": "param [B,F,H+1], mags [B,F,NB], reverb noise/decay/wet",
+            "workload": f"config {args.config} synthesis forward + backward, batch {B}/GPU"}
 
 
 def decoder_leg(args, inp, dev, reps=10):
@@ -313,6 +360,9 @@ def main():
                                  "traffic": traffic.get("harmonic_samples_kernel"),
                                  "kernel": "phase_chunk_sums_kernel + harmonic_samples_kernel<true>",
                                  "avg_launch_ms": round(op_ms, 4)}
+
+    if rank == 0 and not args.no_train_leg:
+        result["train_step"] = train_leg(args, inp, dev)
 
     if rank == 0 and not args.no_decoder_leg:
         result["decoder_forward"] = decoder_leg(args, inp, dev)

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "noise_dsp.h"
@@ -105,194 +106,358 @@ __global__ void __launch_bounds__(256) controls_backward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Harmonic backward, one workgroup per (item, frame).  Item (k, s) of the H x NS grid sums
-// g_t sin(w_t (k+1)) over segment s of the frame's samples; (w_t, g_t) pairs are staged in LDS
-// and read as broadcasts (all lanes of a wave share the segment).
-//   PARAMS: controls recomputed from the raw projection param[B,F,H+1] -> d_param[B,F,H+1]
-//   else:   amp[B,F] and the normalised distribution dist[B,F,H] -> d_amp[B,F], d_dist[B,F,H]
-template <bool PARAMS>
-__global__ void __launch_bounds__(1024) harmonic_backward_kernel(
+// Per-frame backward of the synthesis section, one workgroup per (item, frame).
+//
+// Harmonic part (HMODE 1: frame controls amp[B,F], normalised dist[B,F,H] -> d_amp, d_dist;
+// HMODE 2: raw projection param[B,F,H+1] -> d_param): item (kq, s) of the ceil(H/4) x NS grid
+// sums g_t sin(w_t (k+1)) for the 4 harmonics k = 4kq..4kq+3 over segment s of the frame's
+// samples — one LDS read of the (w_t, g_t) pair feeds 4 sine chains, and all lanes of a wave read
+// the same pair (broadcast).
+//
+// Noise part (NOISE 1: injected noise, 2: Philox regenerated with the forward's counters;
+// RAW: magnitudes are the raw projection, scale_function(m + bias) differentiated too):
+//   dh at the n filter taps by direct correlation of g with the frame's noise — register-blocked
+//   4 taps x 4 lags per step when n/2 % 4 == 0 and n <= bs (the long taps j < n/2 split into
+//   NSEG lag segments, the short wrapped taps one segment each, so the work is even), else one
+//   tap per item; then the transposed filter design, a cosine transform of the windowed tap
+//   gradients folded by the even symmetry of the IR (two threads per band) with the Nyquist band
+//   from an alternating block sum.
+// With both parts (the backward of ddsp_hip_synth_frames) the noise's short LDS phases run beside
+// other workgroups' sine loops, as in the fused forward.
+constexpr int kKPT = 4;  // harmonics per thread
+
+template <int HMODE, int NOISE, bool RAW>
+__global__ void __launch_bounds__(512) frame_backward_kernel(
     const float* __restrict__ f0, const float* __restrict__ grad, const float* __restrict__ param,
     const float* __restrict__ amp, const float* __restrict__ dist, float* __restrict__ d_param,
-    float* __restrict__ d_amp, float* __restrict__ d_dist, int F, int H, int bs, float sr, int NS) {
+    float* __restrict__ d_amp, float* __restrict__ d_dist, int F, int H, int bs, float sr, int NS,
+    const float* __restrict__ mags, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0,
+    uint32_t off1, float bias, float* __restrict__ d_mags, int NB, int NSEG) {
   extern __shared__ float smem[];
   __shared__ double red[32];
   __shared__ double red2[32];
   __shared__ int fast_s;
-  float2* wg = reinterpret_cast<float2*>(smem);  // [bs] (omega_t, g_t)
+  constexpr bool HARM = HMODE != 0;
+  constexpr bool PARAMS = HMODE == 2;
+  // LDS layout (mirrored by frame_backward_lds_floats): xl and gl start 16-B aligned
+  const int hfl = HARM ? 2 * bs + NS * H + H : 0;
+  // (omega_t, g_t) per sample.  (Folding g into per-sample polynomial coefficients, 12 instead of
+  // 13 VALU ops per sine, measured 8% slower: three LDS reads per sample and a larger footprint.)
+  float2* wg = reinterpret_cast<float2*>(smem);  // [bs]
   float* part = smem + 2 * bs;                   // [NS * H]
   float* uk = part + NS * H;                     // [H] u_k (PARAMS: v_k first)
+  const int n = NOISE ? 2 * (NB - 1) : 0, half = n >> 1;
+  const int qmax = min(n, bs);
+  const bool quads = NOISE && (half % 4 == 0) && n <= bs && (bs % 4 == 0);
+  const int npart_len = NSEG * (quads ? n : qmax);
+  float* xl = smem + ((hfl + 3) & ~3);                              // [bs] noise
+  float* ct = xl + bs;                                               // [n] cos(2 pi q / n)
+  float* e = ct + n;                                                 // [n] windowed tap gradients
+  float* npart = e + n;                                              // [npart_len]
+  float* gl = smem + (((xl - smem) + bs + 2 * n + npart_len + 3) & ~3);  // [bs + 8] g, zero-padded
   const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, NT = blockDim.x;
   const int64_t frame = (int64_t)b * F + f;
-  const float* f0b = f0 + (int64_t)b * F;
-  const float pitch0 = f0b[f];
+  const float* gf = grad + frame * bs;
+
+  // ---- phase 1: loads ----
+  double part_s = 0.0, part_d = 0.0;
+  float pitch0 = 0.0f;
   const float half_sr = sr * 0.5f;
   const float* prow = PARAMS ? param + frame * (H + 1) : nullptr;
-
-  double part_s = 0.0, part_d = 0.0;
-  for (int q = tid; q < f; q += NT) part_s += (double)bs * (double)phase_inc(f0b[q], sr);
-  for (int k = tid; k < H; k += NT) {
-    if (PARAMS) {
-      const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
-      uk[k] = v;
-      part_d += (double)v;
-    } else {
-      uk[k] = dist[frame * H + k];
+  if (HARM) {
+    const float* f0b = f0 + (int64_t)b * F;
+    pitch0 = f0b[f];
+    for (int q = tid; q < f; q += NT) part_s += (double)bs * (double)phase_inc(f0b[q], sr);
+    for (int k = tid; k < H; k += NT) {
+      if (PARAMS) {
+        const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+        uk[k] = v;
+        part_d += (double)v;
+      } else {
+        uk[k] = dist[frame * H + k];
+      }
     }
+    for (int j = tid; j < bs; j += NT) wg[j].y = gf[j];
   }
-  const float* gf = grad + frame * bs;
-  for (int j = tid; j < bs; j += NT) wg[j].y = gf[j];
+  if (NOISE) {
+    for (int j = tid; j < bs + 8; j += NT) gl[j] = j < bs ? gf[j] : 0.0f;
+    if (NOISE == 2) {
+      const int fquads = (bs + 3) >> 2;
+      for (int t = tid; t < fquads; t += NT) {
+        const uint64_t qc = (uint64_t)frame * (uint64_t)fquads + (uint64_t)t;
+        const Philox4 r = philox4x32_10((uint32_t)qc, (uint32_t)(qc >> 32), off0, off1, k0, k1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (4 * t + c < bs) xl[4 * t + c] = uniform_pm1(r.v[c]);
+      }
+    } else {
+      const float* xf = noise + frame * bs;
+      for (int j = tid; j < bs; j += NT) xl[j] = xf[j];
+    }
+    fill_cos_table(ct, n);
+  }
   block_sum_double2(part_s, part_d, red);
+
+  // ---- phase 2: phases, normalised distribution ----
   const double S0 = part_s;
   const float norm = (float)part_d;
-  const double dinc = (double)phase_inc(pitch0, sr);
-  for (int j = tid; j < bs; j += NT) wg[j].x = (float)(S0 + (double)(j + 1) * dinc);
-  const float a = PARAMS ? scale_fn(prow[0]) : amp[frame];
-  if (PARAMS)
-    for (int k = tid; k < H; k += NT) uk[k] = uk[k] / norm;
-  if (tid == 0) {
-    const float w0 = (float)(S0 + dinc), w1 = (float)(S0 + (double)bs * dinc);
-    fast_s = fmaxf(fabsf(w0), fabsf(w1)) * (float)H < kFastArgLimit;
+  float a = 0.0f;
+  if (HARM) {
+    const double dinc = (double)phase_inc(pitch0, sr);
+    for (int j = tid; j < bs; j += NT) wg[j].x = (float)(S0 + (double)(j + 1) * dinc);
+    a = PARAMS ? scale_fn(prow[0]) : amp[frame];
+    if (PARAMS)
+      for (int k = tid; k < H; k += NT) uk[k] = uk[k] / norm;
+    if (tid == 0) {
+      const float w0 = (float)(S0 + dinc), w1 = (float)(S0 + (double)bs * dinc);
+      fast_s = fmaxf(fabsf(w0), fabsf(w1)) * (float)H < kFastArgLimit;
+    }
   }
   __syncthreads();
 
-  for (int item = tid; item < H * NS; item += NT) {
-    const int s = item / H, k = item - s * H;
-    const int j0 = (int)((int64_t)s * bs / NS), j1 = (int)((int64_t)(s + 1) * bs / NS);
-    const float kf = (float)(k + 1);
-    float acc0 = 0.0f, acc1 = 0.0f;
-    if (fast_s) {
-      int j = j0;
-      for (; j + 1 < j1; j += 2) {
-        const float2 p0 = wg[j], p1 = wg[j + 1];
-        acc0 = gsin_acc(p0.x * kf, p0.y, acc0);
-        acc1 = gsin_acc(p1.x * kf, p1.y, acc1);
+  // Roles: with both parts the last wave does the noise VJP while the others run the sine
+  // loops (wave specialisation: the noise wave's LDS latency hides under the sine waves' VALU
+  // work); otherwise every thread works on the one part.
+  constexpr bool SPEC = HARM && NOISE != 0;
+  const int NTH = SPEC ? NT - 64 : NT;  // harmonic threads
+  const bool hthread = !SPEC || tid < NTH;
+  const int ntid = SPEC ? tid - NTH : tid, NTN = SPEC ? 64 : NT;  // noise thread id / count
+  const bool nthread = NOISE && (!SPEC || tid >= NTH);
+
+  // ---- phase 3a: harmonic dA_k = sum_t g_t sin(w_t (k+1)) ----
+  if (HARM && hthread) {
+    const int KQ = (H + kKPT - 1) / kKPT;
+    for (int item = tid; item < KQ * NS; item += NTH) {
+      const int s = item / KQ, kq = item - s * KQ;
+      const int j0 = (int)((int64_t)s * bs / NS), j1 = (int)((int64_t)(s + 1) * bs / NS);
+      float kf[kKPT], acc[kKPT];
+#pragma unroll
+      for (int c = 0; c < kKPT; ++c) {
+        kf[c] = (float)(kKPT * kq + c + 1);
+        acc[c] = 0.0f;
       }
-      if (j < j1) acc0 = gsin_acc(wg[j].x * kf, wg[j].y, acc0);
+      if (fast_s) {
+        float acc2[kKPT];
+#pragma unroll
+        for (int c = 0; c < kKPT; ++c) acc2[c] = 0.0f;
+        int j = j0;
+        for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
+          const float2 p = wg[j], p1 = wg[j + 1];
+#pragma unroll
+          for (int c = 0; c < kKPT; ++c) {
+            acc[c] = gsin_acc(p.x * kf[c], p.y, acc[c]);
+            acc2[c] = gsin_acc(p1.x * kf[c], p1.y, acc2[c]);
+          }
+        }
+        if (j < j1) {
+          const float2 p = wg[j];
+#pragma unroll
+          for (int c = 0; c < kKPT; ++c) acc[c] = gsin_acc(p.x * kf[c], p.y, acc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < kKPT; ++c) acc[c] += acc2[c];
+      } else {
+        for (int j = j0; j < j1; ++j) {
+          const float2 p = wg[j];
+#pragma unroll
+          for (int c = 0; c < kKPT; ++c) {
+            const float x = p.x * kf[c];
+            acc[c] = fmaf(p.y, fabsf(x) < kFastArgLimit ? sin_reduced(x) : sin_slow(x), acc[c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < kKPT; ++c)
+        if (kKPT * kq + c < H) part[s * H + kKPT * kq + c] = acc[c];
+    }
+  }
+
+  // ---- phase 3b: the noise VJP (all of it on the noise threads) ----
+  float alt = 0.0f;  // sum_q (-1)^q e[q]  (the Nyquist band)
+  if (nthread) {
+    // local barrier of the noise threads: one wave (LDS is in order per wave) or the workgroup
+    auto nsync = [&]() {
+      if (SPEC) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+      } else {
+        __syncthreads();
+      }
+    };
+    // dh[j(q)] = sum_d g[j+d] x[d]
+    if (quads) {
+      const int nqh = n >> 3;  // quads per half: long (q >= n/2, taps j < n/2) and short
+      const int seglen = ((bs + NSEG - 1) / NSEG + 3) & ~3;
+      for (int item = ntid; item < nqh * NSEG + nqh; item += NTN) {
+        int q0, j0, d0, d1, seg;
+        if (item < nqh * NSEG) {  // long taps: lag range [0, bs - j0) in NSEG segments
+          seg = item / nqh;
+          q0 = half + 4 * (item - seg * nqh);
+          j0 = q0 - half;
+          d0 = seg * seglen;
+          d1 = min(d0 + seglen, bs - j0);
+        } else {  // short (wrapped) taps j0 >= bs - n/2: one segment
+          seg = 0;
+          q0 = 4 * (item - nqh * NSEG);
+          j0 = q0 - half + bs;
+          d0 = 0;
+          d1 = bs - j0;
+        }
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (d0 < d1) {
+          float4 gc = *reinterpret_cast<const float4*>(gl + j0 + d0);
+          int d = d0;
+          for (; d + 4 <= d1; d += 4) {
+            const float4 xv = *reinterpret_cast<const float4*>(xl + d);
+            const float4 gn = *reinterpret_cast<const float4*>(gl + j0 + d + 4);
+            acc.x = fmaf(gc.x, xv.x, fmaf(gc.y, xv.y, fmaf(gc.z, xv.z, fmaf(gc.w, xv.w, acc.x))));
+            acc.y = fmaf(gc.y, xv.x, fmaf(gc.z, xv.y, fmaf(gc.w, xv.z, fmaf(gn.x, xv.w, acc.y))));
+            acc.z = fmaf(gc.z, xv.x, fmaf(gc.w, xv.y, fmaf(gn.x, xv.z, fmaf(gn.y, xv.w, acc.z))));
+            acc.w = fmaf(gc.w, xv.x, fmaf(gn.x, xv.y, fmaf(gn.y, xv.z, fmaf(gn.z, xv.w, acc.w))));
+            gc = gn;
+          }
+          for (; d < d1; ++d) {  // g is zero past bs, so taps c > 0 need no separate bound
+            const float xv = xl[d];
+            acc.x = fmaf(gl[j0 + d], xv, acc.x);
+            acc.y = fmaf(gl[j0 + d + 1], xv, acc.y);
+            acc.z = fmaf(gl[j0 + d + 2], xv, acc.z);
+            acc.w = fmaf(gl[j0 + d + 3], xv, acc.w);
+          }
+        }
+        float* dst = npart + seg * n + q0;
+        dst[0] = acc.x;
+        dst[1] = acc.y;
+        dst[2] = acc.z;
+        dst[3] = acc.w;
+      }
     } else {
-      for (int j = j0; j < j1; ++j) {
-        const float x = wg[j].x * kf;
-        acc0 = fmaf(wg[j].y, fabsf(x) < kFastArgLimit ? sin_reduced(x) : sin_slow(x), acc0);
+      for (int item = ntid; item < qmax * NSEG; item += NTN) {
+        const int seg = item / qmax, q = item - seg * qmax;
+        int j = (q - half) % bs;
+        if (j < 0) j += bs;
+        const int d0 = (int)((int64_t)seg * bs / NSEG);
+        const int d1 = min((int)((int64_t)(seg + 1) * bs / NSEG), bs - j);
+        float c0 = 0.0f, c1 = 0.0f;
+        int d = d0;
+        for (; d + 1 < d1; d += 2) {
+          c0 = fmaf(gl[j + d], xl[d], c0);
+          c1 = fmaf(gl[j + d + 1], xl[d + 1], c1);
+        }
+        if (d < d1) c0 = fmaf(gl[j + d], xl[d], c0);
+        npart[seg * qmax + q] = c0 + c1;
       }
     }
-    part[s * H + k] = acc0 + acc1;
-  }
-  __syncthreads();
-
-  double da_part = 0.0;
-  for (int k = tid; k < H; k += NT) {
-    float dA = part[k];
-    for (int s = 1; s < NS; ++s) dA += part[s * H + k];
-    part[k] = dA;
-    da_part += (double)dA * (double)uk[k];
-  }
-  const float da = (float)block_sum_double(da_part, red2);  // barrier: part[0..H) complete
-  if (PARAMS) {
-    float* dp = d_param + frame * (H + 1);
-    for (int k = tid; k < H; k += NT) {
-      const float mask = (pitch0 * (float)(k + 1)) < half_sr ? kOnePlusEps : kEps;
-      const float dv = a * (part[k] - da) / norm;
-      dp[1 + k] = dv * mask * scale_fn_grad(prow[1 + k]);
+    nsync();
+    // e[q] = dh[j(q)] hann[q]; the alternating sum for the Nyquist band
+    double alt_part = 0.0;
+    for (int q = ntid; q < n; q += NTN) {
+      float v = 0.0f;
+      if (q < qmax) {
+        if (quads) {
+          const int ns_q = q >= half ? NSEG : 1;
+          for (int s = 0; s < ns_q; ++s) v += npart[s * n + q];
+        } else {
+          for (int s = 0; s < NSEG; ++s) v += npart[s * qmax + q];
+        }
+        v *= 0.5f - 0.5f * ct[q];  // periodic Hann(n) at q
+      }
+      e[q] = v;
+      alt_part += (q & 1) ? -(double)v : (double)v;
     }
-    if (tid == 0) dp[0] = da * scale_fn_grad(prow[0]);
-  } else {
-    for (int k = tid; k < H; k += NT) d_dist[frame * H + k] = part[k] * a;
-    if (tid == 0) d_amp[frame] = da;
+    if (SPEC) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) alt_part += __shfl_xor(alt_part, o, 64);
+    } else {
+      alt_part = block_sum_double(alt_part, red2);  // includes the barrier publishing e[]
+    }
+    alt = (float)alt_part;
+    nsync();
+    // dA_k = (c_k/n)(-1)^k [e0 + (-1)^k e_half + sum_{q=1}^{half-1} (e_q + e_{n-q}) cos(2 pi q k/n)],
+    // k < half on two threads (q halves) each; k = half from the alternating sum.
+    float* dAp = npart;  // [2][half] (npart is consumed)
+    const int mid = (half + 1) >> 1;
+    const bool pow2 = (n & (n - 1)) == 0;
+    for (int item = ntid; item < 2 * half; item += NTN) {
+      const int pr = item / half, k = item - pr * half;
+      const int q0 = pr ? mid : 1, q1 = pr ? half : mid;
+      float s0 = 0.0f, s1 = 0.0f;
+      if (pow2) {
+        const int mask = n - 1;
+        int q = q0;
+        for (; q + 1 < q1; q += 2) {
+          s0 = fmaf(e[q] + e[n - q], ct[(q * k) & mask], s0);
+          s1 = fmaf(e[q + 1] + e[n - q - 1], ct[((q + 1) * k) & mask], s1);
+        }
+        if (q < q1) s0 = fmaf(e[q] + e[n - q], ct[(q * k) & mask], s0);
+      } else {
+        int qk = (int)(((int64_t)q0 * k) % n);
+        for (int q = q0; q < q1; ++q) {
+          s0 = fmaf(e[q] + e[n - q], ct[qk], s0);
+          qk += k;
+          if (qk >= n) qk -= n;
+        }
+      }
+      float v = s0 + s1;
+      if (pr == 0) v += e[0] + ((k & 1) ? -e[half] : e[half]);
+      dAp[pr * half + k] = v;
+    }
+    nsync();
+    const float inv_n = 1.0f / (float)n;
+    for (int k = ntid; k < NB; k += NTN) {
+      float dA = k < half ? (dAp[k] + dAp[half + k]) * (k == 0 ? 1.0f : 2.0f) * inv_n : alt * inv_n;
+      if (k & 1) dA = -dA;
+      d_mags[frame * NB + k] = RAW ? dA * scale_fn_grad(mags[frame * NB + k] + bias) : dA;
+    }
+  }
+
+  if (HARM) {
+    // ---- phase 4: harmonic reductions and outputs ----
+    __syncthreads();
+    double da_part = 0.0;
+    for (int k = tid; k < H; k += NT) {
+      float dA = part[k];
+      for (int s = 1; s < NS; ++s) dA += part[s * H + k];
+      part[k] = dA;
+      da_part += (double)dA * (double)uk[k];
+    }
+    const float da = (float)block_sum_double(da_part, red2);  // barrier: part[0..H) complete
+    if (PARAMS) {
+      float* dp = d_param + frame * (H + 1);
+      for (int k = tid; k < H; k += NT) {
+        const float mask = (pitch0 * (float)(k + 1)) < half_sr ? kOnePlusEps : kEps;
+        const float dv = a * (part[k] - da) / norm;
+        dp[1 + k] = dv * mask * scale_fn_grad(prow[1 + k]);
+      }
+      if (tid == 0) dp[0] = da * scale_fn_grad(prow[0]);
+    } else {
+      for (int k = tid; k < H; k += NT) d_dist[frame * H + k] = part[k] * a;
+      if (tid == 0) d_amp[frame] = da;
+    }
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Filtered-noise backward, one workgroup per frame: dh at the n filter taps by direct
-// correlation of g with the frame's noise (NSEG segments of the lag sum per tap), then the
-// transposed filter design (a cosine transform of the windowed tap gradients) -> dA [NB].
-//   RNG: the noise is regenerated from the forward's Philox (seed, offset) — same counter
-//   mapping as filtered_noise_kernel / synth_frame_kernel;  RAW: chain scale_fn(m + bias).
-template <bool RNG, bool RAW>
-__global__ void __launch_bounds__(256) noise_backward_kernel(
-    const float* __restrict__ grad, const float* __restrict__ noise, uint32_t k0, uint32_t k1,
-    uint32_t off0, uint32_t off1, const float* __restrict__ mags, float bias, float* __restrict__ d_mags,
-    int NB, int bs, int NSEG) {
-  extern __shared__ float smem[];
-  const int n = 2 * (NB - 1), half = n >> 1;
-  const int qmax = min(n, bs);
-  float* gl = smem;            // [bs]
-  float* xl = gl + bs;         // [bs]
-  float* ct = xl + bs;         // [n]
-  float* e = ct + n;           // [n]   windowed tap gradients by q
-  float* part = e + n;         // [NSEG * qmax]
-  const int64_t frame = blockIdx.x;
-  const int tid = threadIdx.x, NT = blockDim.x;
-  const float* gf = grad + frame * bs;
-  for (int j = tid; j < bs; j += NT) gl[j] = gf[j];
-  if (RNG) {
-    const int fquads = (bs + 3) >> 2;
-    for (int t = tid; t < fquads; t += NT) {
-      const uint64_t qc = (uint64_t)frame * (uint64_t)fquads + (uint64_t)t;
-      const Philox4 r = philox4x32_10((uint32_t)qc, (uint32_t)(qc >> 32), off0, off1, k0, k1);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (4 * t + c < bs) xl[4 * t + c] = uniform_pm1(r.v[c]);
-    }
-  } else {
-    const float* xf = noise + frame * bs;
-    for (int j = tid; j < bs; j += NT) xl[j] = xf[j];
-  }
-  fill_cos_table(ct, n);
-  __syncthreads();
+// LDS floats of frame_backward_kernel (its layout, written out on the host)
+size_t frame_backward_lds_floats(bool harm, bool noise, int H, int bs, int NS, int NB, int NSEG) {
+  const size_t hfl = harm ? (size_t)2 * bs + (size_t)NS * H + H : 0;
+  if (!noise) return hfl;
+  const int n = 2 * (NB - 1);
+  const int qmax = std::min(n, bs);
+  const bool quads = ((n / 2) % 4 == 0) && n <= bs && bs % 4 == 0;
+  const size_t npart_len = (size_t)NSEG * (quads ? n : qmax);
+  const size_t off_xl = (hfl + 3) & ~(size_t)3;
+  const size_t off_gl = (off_xl + (size_t)bs + 2 * (size_t)n + npart_len + 3) & ~(size_t)3;
+  return off_gl + (size_t)bs + 8;
+}
 
-  // dh[j(q)] = sum_{d=0}^{bs-1-j} g[j+d] x[d], lag range split into NSEG fixed d-segments
-  for (int item = tid; item < qmax * NSEG; item += NT) {
-    const int seg = item / qmax, q = item - seg * qmax;
-    int j = (q - half) % bs;
-    if (j < 0) j += bs;
-    const int d0 = (int)((int64_t)seg * bs / NSEG);
-    const int d1 = min((int)((int64_t)(seg + 1) * bs / NSEG), bs - j);
-    float c0 = 0.0f, c1 = 0.0f;
-    int d = d0;
-    for (; d + 1 < d1; d += 2) {
-      c0 = fmaf(gl[j + d], xl[d], c0);
-      c1 = fmaf(gl[j + d + 1], xl[d + 1], c1);
-    }
-    if (d < d1) c0 = fmaf(gl[j + d], xl[d], c0);
-    part[seg * qmax + q] = c0 + c1;
+// noise lag segments: per long tap quad on the register-blocked path, else per tap
+int noise_nseg(int nt, int NB, int bs) {
+  const int n = 2 * (NB - 1);
+  const bool quads = ((n / 2) % 4 == 0) && n <= bs && bs % 4 == 0;
+  if (quads) {
+    const int nqh = n / 8;
+    return std::max(1, std::min(16, (nt - nqh) / std::max(nqh, 1)));
   }
-  __syncthreads();
-  for (int q = tid; q < n; q += NT) {
-    float v = 0.0f;
-    if (q < qmax) {
-      for (int s = 0; s < NSEG; ++s) v += part[s * qmax + q];
-      v *= 0.5f - 0.5f * ct[q];  // periodic Hann(n) at q
-    }
-    e[q] = v;
-  }
-  __syncthreads();
-
-  const float inv_n = 1.0f / (float)n;
-  const bool pow2 = (n & (n - 1)) == 0;
-  for (int k = tid; k < NB; k += NT) {
-    float s0 = 0.0f, s1 = 0.0f;
-    if (pow2) {
-      const int mask = n - 1;
-      int q = 0;
-      for (; q + 1 < n; q += 2) {
-        s0 = fmaf(e[q], ct[(q * k) & mask], s0);
-        s1 = fmaf(e[q + 1], ct[((q + 1) * k) & mask], s1);
-      }
-      for (; q < n; ++q) s0 = fmaf(e[q], ct[(q * k) & mask], s0);
-    } else {
-      int qk = 0;
-      for (int q = 0; q < n; ++q) {
-        s0 = fmaf(e[q], ct[qk], s0);
-        qk += k;
-        if (qk >= n) qk -= n;
-      }
-    }
-    const float ck = (k == 0 || k == half) ? 1.0f : 2.0f;
-    float dA = (s0 + s1) * ck * inv_n;
-    if (k & 1) dA = -dA;
-    if (RAW) dA *= scale_fn_grad(mags[frame * NB + k] + bias);
-    d_mags[frame * NB + k] = dA;
-  }
+  return std::max(1, std::min(8, nt / std::max(std::min(n, bs), 1)));
 }
 
 // amp_to_impulse_response backward (core.py:144-166): dimpulse[rows, target] -> damp[rows, NB]
@@ -365,26 +530,22 @@ unsigned grid1d(int64_t n, int per_block) {
   return (unsigned)std::min<int64_t>(std::max<int64_t>((n + per_block - 1) / per_block, 1), 1 << 20);
 }
 
-// NS sample segments per harmonic for the harmonic backward: fill the workgroup's waves.
+// Harmonic backward geometry: NS sample segments so that ceil(H/4) x NS fills about
+// kBwdThreads threads (small workgroups: several per CU hide each one's latency-bound phases).
+int bwd_threads() {
+  static int v = [] {
+    const char* e = getenv("DDSP_HIP_BWD_THREADS");  // tuning knob (64..512)
+    const int t = e ? atoi(e) : 128;  // measured best at config 2 (64..512 swept)
+    return std::max(64, std::min(512, (t / 64) * 64));
+  }();
+  return v;
+}
+
 void harmonic_backward_shape(int H, int bs, int& nt, int& ns) {
-  double best = -1.0;
-  nt = 64;
-  ns = 1;
-  for (int s = 1; s <= 8 && s <= bs; ++s) {
-    const int items = H * s;
-    if (items > 1024) break;
-    const int t = ((items + 63) / 64) * 64;
-    const double eff = (double)items / (double)t;
-    if (eff > best + 1e-9) {
-      best = eff;
-      nt = t;
-      ns = s;
-    }
-  }
-  if (H > 1024) {
-    nt = 1024;
-    ns = 1;
-  }
+  const int kq = (H + kKPT - 1) / kKPT;
+  const int target = bwd_threads();
+  ns = std::max(1, std::min(std::min(target / kq, bs), 64));
+  nt = std::min(512, ((kq * ns + 63) / 64) * 64);
 }
 
 }  // namespace
@@ -432,24 +593,48 @@ int ddsp_hip_harmonic_controls_backward(const float* amplitudes_raw, int64_t amp
   return launch_status();
 }
 
-static int harmonic_backward_launch(bool params, const float* f0, const float* grad, const float* param,
-                                    const float* amp, const float* dist, float* d_param, float* d_amp,
-                                    float* d_dist, int64_t batch, int64_t frames, int64_t H, int64_t bs,
-                                    float sr, void* stream) {
-  if (batch < 0 || frames < 0 || H < 1 || bs < 1 || !(sr > 0)) return DDSP_HIP_EINVAL;
+// hmode: 0 no harmonic part, 1 frame controls, 2 raw params; noise_mode: 0 none, 1 injected, 2 Philox
+static int frame_backward_launch(int hmode, int noise_mode, bool raw, const float* f0, const float* grad,
+                                 const float* param, const float* amp, const float* dist, float* d_param,
+                                 float* d_amp, float* d_dist, int64_t batch, int64_t frames, int64_t H,
+                                 int64_t bs, float sr, const float* mags, const float* noise, uint64_t seed,
+                                 uint64_t offset, float bias, float* d_mags, int64_t NB, void* stream) {
+  if (batch < 0 || frames < 0 || bs < 1 || (hmode && (H < 1 || !(sr > 0)))) return DDSP_HIP_EINVAL;
+  if (noise_mode && NB < 2) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
-  if (batch > 65535 || frames > INT32_MAX || H > 4096 || bs > 8192) return DDSP_HIP_ERANGE;
-  int nt, ns;
-  harmonic_backward_shape((int)H, (int)bs, nt, ns);
-  const size_t shm = sizeof(float) * ((size_t)2 * bs + (size_t)ns * H + H);
+  if (batch > 65535 || frames > INT32_MAX || H > 4096 || bs > 8192 || NB > 4097) return DDSP_HIP_ERANGE;
+  int nt = 128, ns = 1;
+  if (hmode) harmonic_backward_shape((int)H, (int)bs, nt, ns);
+  // both parts: one extra wave runs the noise VJP beside the sine waves
+  const bool spec = hmode && noise_mode;
+  const int nseg = noise_mode ? noise_nseg(spec ? 64 : nt, (int)NB, (int)bs) : 0;
+  if (spec) nt += 64;
+  const size_t shm = sizeof(float) * frame_backward_lds_floats(hmode != 0, noise_mode != 0, (int)H, (int)bs, ns,
+                                                               (int)NB, nseg);
   if (shm > 150 * 1024) return DDSP_HIP_ERANGE;
   const dim3 grid((unsigned)frames, (unsigned)batch);
-  if (params)
-    hipLaunchKernelGGL(harmonic_backward_kernel<true>, grid, dim3(nt), shm, S(stream), f0, grad, param, nullptr,
-                       nullptr, d_param, nullptr, nullptr, (int)frames, (int)H, (int)bs, sr, ns);
-  else
-    hipLaunchKernelGGL(harmonic_backward_kernel<false>, grid, dim3(nt), shm, S(stream), f0, grad, nullptr, amp,
-                       dist, nullptr, d_amp, d_dist, (int)frames, (int)H, (int)bs, sr, ns);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
+#define DDSP_FB_LAUNCH(HM_, N_, R_)                                                                         \
+  hipLaunchKernelGGL((frame_backward_kernel<HM_, N_, R_>), grid, dim3(nt), shm, S(stream), f0, grad, param, amp, \
+                     dist, d_param, d_amp, d_dist, (int)frames, (int)H, (int)bs, sr, ns, mags, noise, k0, k1,  \
+                     o0, o1, bias, d_mags, (int)NB, nseg)
+  if (hmode == 1 && noise_mode == 0) {
+    DDSP_FB_LAUNCH(1, 0, false);
+  } else if (hmode == 2 && noise_mode == 0) {
+    DDSP_FB_LAUNCH(2, 0, false);
+  } else if (hmode == 2 && noise_mode == 1 && raw) {
+    DDSP_FB_LAUNCH(2, 1, true);
+  } else if (hmode == 2 && noise_mode == 2 && raw) {
+    DDSP_FB_LAUNCH(2, 2, true);
+  } else if (hmode == 0 && noise_mode == 1) {
+    if (raw) DDSP_FB_LAUNCH(0, 1, true); else DDSP_FB_LAUNCH(0, 1, false);
+  } else if (hmode == 0 && noise_mode == 2) {
+    if (raw) DDSP_FB_LAUNCH(0, 2, true); else DDSP_FB_LAUNCH(0, 2, false);
+  } else {
+    return DDSP_HIP_EINVAL;
+  }
+#undef DDSP_FB_LAUNCH
   return launch_status();
 }
 
@@ -460,8 +645,9 @@ int ddsp_hip_harmonic_synth_frames_backward(const float* f0, const float* amplit
                                             void* stream) {
   if (!f0 || !amplitudes || !distribution || !grad || !grad_amplitudes || !grad_distribution)
     return batch == 0 || frames == 0 ? DDSP_HIP_OK : DDSP_HIP_EINVAL;
-  return harmonic_backward_launch(false, f0, grad, nullptr, amplitudes, distribution, nullptr, grad_amplitudes,
-                                  grad_distribution, batch, frames, n_harmonic, block_size, sample_rate, stream);
+  return frame_backward_launch(1, 0, false, f0, grad, nullptr, amplitudes, distribution, nullptr, grad_amplitudes,
+                               grad_distribution, batch, frames, n_harmonic, block_size, sample_rate, nullptr,
+                               nullptr, 0, 0, 0.0f, nullptr, 0, stream);
 }
 
 int ddsp_hip_harmonic_synth_params_backward(const float* f0, const float* param, const float* grad,
@@ -469,8 +655,30 @@ int ddsp_hip_harmonic_synth_params_backward(const float* f0, const float* param,
                                             int64_t n_harmonic, int64_t block_size, float sample_rate,
                                             void* stream) {
   if (!f0 || !param || !grad || !grad_param) return batch == 0 || frames == 0 ? DDSP_HIP_OK : DDSP_HIP_EINVAL;
-  return harmonic_backward_launch(true, f0, grad, param, nullptr, nullptr, grad_param, nullptr, nullptr, batch,
-                                  frames, n_harmonic, block_size, sample_rate, stream);
+  return frame_backward_launch(2, 0, false, f0, grad, param, nullptr, nullptr, grad_param, nullptr, nullptr, batch,
+                               frames, n_harmonic, block_size, sample_rate, nullptr, nullptr, 0, 0, 0.0f, nullptr, 0,
+                               stream);
+}
+
+int ddsp_hip_synth_frames_backward(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                   const float* noise, uint64_t seed, uint64_t offset, const float* grad_harmonic,
+                                   const float* grad_noise, float* grad_param, float* grad_magnitudes,
+                                   int64_t batch, int64_t frames, int64_t n_harmonic, int64_t n_bands,
+                                   int64_t block_size, float sample_rate, void* stream) {
+  if (batch == 0 || frames == 0) return batch < 0 || frames < 0 ? DDSP_HIP_EINVAL : DDSP_HIP_OK;
+  if (!f0 || !param || !raw_magnitudes || !grad_harmonic || !grad_param || !grad_magnitudes)
+    return DDSP_HIP_EINVAL;
+  if (grad_noise && grad_noise != grad_harmonic) {  // distinct upstream gradients: two passes
+    int st = frame_backward_launch(2, 0, false, f0, grad_harmonic, param, nullptr, nullptr, grad_param, nullptr,
+                                   nullptr, batch, frames, n_harmonic, block_size, sample_rate, nullptr, nullptr, 0,
+                                   0, 0.0f, nullptr, 0, stream);
+    if (st) return st;
+    return ddsp_hip_filtered_noise_backward(raw_magnitudes, noise, seed, offset, 1, bias, grad_noise,
+                                            grad_magnitudes, batch, frames, n_bands, block_size, stream);
+  }
+  return frame_backward_launch(2, noise ? 1 : 2, true, f0, grad_harmonic, param, nullptr, nullptr, grad_param,
+                               nullptr, nullptr, batch, frames, n_harmonic, block_size, sample_rate, raw_magnitudes,
+                               noise, seed, offset, bias, grad_magnitudes, n_bands, stream);
 }
 
 int ddsp_hip_filtered_noise_backward(const float* magnitudes, const float* noise, uint64_t seed, uint64_t offset,
@@ -478,29 +686,11 @@ int ddsp_hip_filtered_noise_backward(const float* magnitudes, const float* noise
                                      int64_t batch, int64_t frames, int64_t n_bands, int64_t block_size,
                                      void* stream) {
   if (batch < 0 || frames < 0 || n_bands < 2 || block_size < 1) return DDSP_HIP_EINVAL;
-  const int64_t nf = batch * frames;
-  if (nf == 0) return DDSP_HIP_OK;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
   if (!grad || !grad_magnitudes || (raw && !magnitudes)) return DDSP_HIP_EINVAL;
-  if (nf > INT32_MAX || block_size > 8192 || n_bands > 4097) return DDSP_HIP_ERANGE;
-  const int n = 2 * (int)(n_bands - 1), bs = (int)block_size;
-  const int qmax = std::min(n, bs);
-  const int nt = 256;
-  const int nseg = std::max(1, std::min(8, nt / qmax));
-  const size_t shm = sizeof(float) * ((size_t)2 * bs + 2 * (size_t)n + (size_t)nseg * qmax);
-  if (shm > 150 * 1024) return DDSP_HIP_ERANGE;
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
-  const dim3 grid((unsigned)nf);
-#define DDSP_NB_LAUNCH(RNG_, RAW_)                                                                            \
-  hipLaunchKernelGGL((noise_backward_kernel<RNG_, RAW_>), grid, dim3(nt), shm, S(stream), grad, noise, k0, k1, o0, \
-                     o1, magnitudes, bias, grad_magnitudes, (int)n_bands, bs, nseg)
-  if (noise) {
-    if (raw) DDSP_NB_LAUNCH(false, true); else DDSP_NB_LAUNCH(false, false);
-  } else {
-    if (raw) DDSP_NB_LAUNCH(true, true); else DDSP_NB_LAUNCH(true, false);
-  }
-#undef DDSP_NB_LAUNCH
-  return launch_status();
+  return frame_backward_launch(0, noise ? 1 : 2, raw != 0, nullptr, grad, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               nullptr, batch, frames, 0, block_size, 0.0f, magnitudes, noise, seed, offset, bias,
+                               grad_magnitudes, n_bands, stream);
 }
 
 int ddsp_hip_amp_to_impulse_response_backward(const float* grad_impulse, float* grad_amp, int64_t rows,

@@ -48,19 +48,23 @@ __global__ void build_impulse_kernel(const float* __restrict__ noise, const floa
 
 // Reverb.build_impulse backward (modules.py:21-26): imp[i] = noise[i] env[i] w (i >= 1),
 // env = exp(-softplus(-decay) t 500), w = sigmoid(wet); imp[0] = 1 carries no gradient.
-// Taps i >= grad_len (cropped away by a shorter input) have zero gradient.  One workgroup.
-__global__ void __launch_bounds__(1024) impulse_backward_kernel(
+// Taps i >= grad_len (cropped away by a shorter input) have zero gradient.
+// Pass 1 (grid-stride over the taps): d_noise and per-workgroup fp64 partial sums of
+// sum dimp*noise*env and sum dimp*noise*env*t; pass 2 (one workgroup) reduces them in a fixed
+// order (deterministic) into d_wet and d_decay.
+constexpr int kImpBlocks = 128;
+
+__global__ void __launch_bounds__(256) impulse_backward_kernel(
     const float* __restrict__ noise, const float* __restrict__ decay, const float* __restrict__ wet,
     const float* __restrict__ dimp, int64_t grad_len, int64_t L, float sr, float* __restrict__ d_noise,
-    float* __restrict__ d_decay, float* __restrict__ d_wet) {
+    double* __restrict__ partials) {
   __shared__ double red[32];
   const float d = -decay[0];
   const float sp = d > 20.0f ? d : log1pf(expf(d));
-  const float spg = d > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-d));  // softplus'(d)
   const float neg = -sp;
   const float w = 1.0f / (1.0f + expf(-wet[0]));
   double aw = 0.0, ad = 0.0;
-  for (int64_t i = threadIdx.x; i < L; i += blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L; i += (int64_t)gridDim.x * blockDim.x) {
     const float t = (float)i / sr;
     const float env = expf((neg * t) * 500.0f);
     const float gi = (i >= 1 && i < grad_len) ? dimp[i] : 0.0f;
@@ -71,9 +75,27 @@ __global__ void __launch_bounds__(1024) impulse_backward_kernel(
   }
   block_sum_double2(aw, ad, red);
   if (threadIdx.x == 0) {
-    d_wet[0] = (float)(aw * (double)w * (1.0 - (double)w));
-    d_decay[0] = (float)(ad * (double)w * 500.0 * (double)spg);
+    partials[2 * blockIdx.x] = aw;
+    partials[2 * blockIdx.x + 1] = ad;
   }
+}
+
+__global__ void __launch_bounds__(64) impulse_backward_finish_kernel(const double* __restrict__ partials, int nblk,
+                                                                     const float* __restrict__ decay,
+                                                                     const float* __restrict__ wet,
+                                                                     float* __restrict__ d_decay,
+                                                                     float* __restrict__ d_wet) {
+  if (threadIdx.x != 0) return;
+  double aw = 0.0, ad = 0.0;
+  for (int i = 0; i < nblk; ++i) {
+    aw += partials[2 * i];
+    ad += partials[2 * i + 1];
+  }
+  const float d = -decay[0];
+  const float spg = d > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-d));  // softplus'(d)
+  const float w = 1.0f / (1.0f + expf(-wet[0]));
+  d_wet[0] = (float)(aw * (double)w * (1.0 - (double)w));
+  d_decay[0] = (float)(ad * (double)w * 500.0 * (double)spg);
 }
 
 unsigned grid_for(int64_t n) {
@@ -154,15 +176,27 @@ int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impul
   return upols_corr(x, grad, batch, n_samples, ir_length, grad_impulse, workspace, workspace_bytes, stream);
 }
 
+size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length) {
+  (void)length;
+  return 2 * sizeof(double) * kImpBlocks;
+}
+
 int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
                                      const float* grad_impulse, int64_t length, int64_t grad_length,
                                      float sample_rate, float* grad_noise, float* grad_decay, float* grad_wet,
-                                     void* stream) {
+                                     void* workspace, size_t workspace_bytes, void* stream) {
   if (length < 1 || grad_length < 0 || !noise || !decay || !wet || !grad_impulse || !grad_noise ||
       !grad_decay || !grad_wet || !(sample_rate > 0))
     return DDSP_HIP_EINVAL;
-  hipLaunchKernelGGL(impulse_backward_kernel, dim3(1), dim3(1024), 0, S(stream), noise, decay, wet,
-                     grad_impulse, std::min(grad_length, length), length, sample_rate, grad_noise,
+  if (!workspace || workspace_bytes < ddsp_hip_reverb_impulse_backward_workspace_size(length))
+    return DDSP_HIP_EWORKSPACE;
+  const int nblk = (int)std::min<int64_t>(kImpBlocks, (length + 255) / 256);
+  double* partials = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(impulse_backward_kernel, dim3(nblk), dim3(256), 0, S(stream), noise, decay, wet,
+                     grad_impulse, std::min(grad_length, length), length, sample_rate, grad_noise, partials);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(impulse_backward_finish_kernel, dim3(1), dim3(64), 0, S(stream), partials, nblk, decay, wet,
                      grad_decay, grad_wet);
   return launch_status();
 }

@@ -282,14 +282,19 @@ class SynthFramesFn(_F):
     @staticmethod
     def backward(ctx, g_out, g_harm=None, g_nz=None):
         f0, param, mags = ctx.saved_tensors
-        gh = g_out if g_harm is None else g_out + g_harm
-        gn = g_out if g_nz is None else g_out + g_nz
-        dp = dm = None
-        if ctx.needs_input_grad[1]:
-            dp = params_backward(f0.detach(), param.detach(), _g(gh), ctx.bs, ctx.sr)
-        if ctx.needs_input_grad[2]:
-            dm = noise_backward(mags.detach(), ctx.noise, ctx.seed, ctx.offset, ctx.bias, _g(gn), ctx.bs)
-        return None, dp, dm, None, None, None, None, None
+        gh = _g(g_out if g_harm is None else g_out + g_harm)
+        gn = None if g_nz is None else _g(g_out + g_nz)
+        B, F, H1 = param.shape
+        NB = mags.shape[-1]
+        dp = torch.empty(B, F, H1, dtype=torch.float32, device=param.device)
+        dm = torch.empty(B, F, NB, dtype=torch.float32, device=param.device)
+        # one launch for both halves (the noise VJP fused into the harmonic one)
+        _lib.call("synth_frames_backward", _lib.ptr(core._c(f0.detach())), _lib.ptr(core._c(param.detach())),
+                  _lib.ptr(core._c(mags.detach())), ctx.bias, _lib.ptr(ctx.noise), ctx.seed, ctx.offset,
+                  _lib.ptr(gh), _lib.ptr(gn), _lib.ptr(dp), _lib.ptr(dm), B, F, H1 - 1, NB, ctx.bs, ctx.sr,
+                  _lib.stream_of(dp))
+        return (None, dp if ctx.needs_input_grad[1] else None, dm if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None)
 
 
 # ------------------------------------------------------------------------------------------
@@ -316,9 +321,10 @@ def impulse_backward(noise, decay, wet, dimp, grad_length, sample_rate):
     dn = torch.empty_like(core._c(noise))
     dd = torch.empty((), dtype=torch.float32, device=noise.device)
     dw = torch.empty((), dtype=torch.float32, device=noise.device)
+    ws = core._workspace(_lib.query("reverb_impulse_backward_workspace_size", L), noise.device)
     _lib.call("reverb_impulse_backward", _lib.ptr(core._c(noise)), _lib.ptr(core._c(decay)), _lib.ptr(core._c(wet)),
               _lib.ptr(dimp), L, int(grad_length), float(sample_rate), _lib.ptr(dn), _lib.ptr(dd), _lib.ptr(dw),
-              _lib.stream_of(dn))
+              _lib.ptr(ws), ws.numel(), _lib.stream_of(dn))
     return dn.reshape(noise.shape), dd.reshape(decay.shape), dw.reshape(wet.shape)
 
 

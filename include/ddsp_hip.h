@@ -207,6 +207,16 @@ int ddsp_hip_harmonic_synth_params_backward(const float* f0, const float* param,
                                             int64_t n_harmonic, int64_t block_size, float sample_rate,
                                             void* stream);
 
+/* decoder.py:106-121 backward (ddsp_hip_synth_frames): one launch computes grad_param[B,F,H+1] and
+ * grad_magnitudes[B,F,NB] (raw projections) from the upstream gradient of the signal; the noise
+ * is `noise` or the forward's Philox (seed, offset).  grad_noise (nullable) is a separate upstream
+ * gradient for the noise half (when the parts are used separately); NULL = grad_harmonic. */
+int ddsp_hip_synth_frames_backward(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                   const float* noise, uint64_t seed, uint64_t offset, const float* grad_harmonic,
+                                   const float* grad_noise, float* grad_param, float* grad_magnitudes,
+                                   int64_t batch, int64_t frames, int64_t n_harmonic, int64_t n_bands,
+                                   int64_t block_size, float sample_rate, void* stream);
+
 /* modules.py:111-128 FilteredNoise backward (ddsp_hip_filtered_noise[_params], the noise half of
  * ddsp_hip_synth_frames): grad[B,F*bs] -> grad_magnitudes[B,F,NB].  The noise is `noise` as given
  * to the forward, or (noise == NULL) regenerated from the forward's (seed, offset).  raw != 0:
@@ -230,10 +240,11 @@ size_t ddsp_hip_reverb_ir_grad_workspace_size(int64_t batch, int64_t n_samples, 
 int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impulse, int64_t batch,
                             int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
                             void* stream);
+size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length);
 int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
                                      const float* grad_impulse, int64_t length, int64_t grad_length,
                                      float sample_rate, float* grad_noise, float* grad_decay, float* grad_wet,
-                                     void* stream);
+                                     void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }
