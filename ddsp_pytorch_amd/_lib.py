@@ -58,8 +58,9 @@ SIGNATURES = {
                                             _I64, _I64, _F, _P]),
     "ddsp_hip_filtered_noise_backward": (_I, [_P, _P, _U64, _U64, _I, _F, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "ddsp_hip_reverb_apply_transposed": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
-    "ddsp_hip_reverb_ir_grad_workspace_size": (_SZ, [_I64, _I64, _I64]),
-    "ddsp_hip_reverb_ir_grad": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_reverb_input_spectra_bytes": (_SZ, [_I64, _I64]),
+    "ddsp_hip_reverb_backward_workspace_size": (_SZ, [_I64, _I64, _I64, _I]),
+    "ddsp_hip_reverb_backward": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_reverb_impulse_backward_workspace_size": (_SZ, [_I64]),
     "ddsp_hip_reverb_impulse_backward": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _P, _P, _P, _P, _SZ, _P]),
 }

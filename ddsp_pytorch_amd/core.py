@@ -434,6 +434,12 @@ def reverb_apply(x, spectrum, ir_length):
             raise NotImplementedError("reverb_apply: the IR spectrum is not differentiable; use "
                                       "modules.Reverb (gradients for noise/decay/wet) instead")
         return _grad.ReverbApplyFn.apply(x, spectrum, int(ir_length))
+    return _reverb_apply_launch(x, spectrum, ir_length)[0]
+
+
+def _reverb_apply_launch(x, spectrum, ir_length):
+    """-> (out, workspace); on return the workspace's first reverb_input_spectra_bytes hold x's
+    partition spectra (reused by the backward)."""
     B, T = x.shape[0], x.shape[1]
     if spectrum.numel() != reverb_spectrum_floats(T, ir_length):
         raise RuntimeError("reverb_apply: spectrum was computed for a different length")
@@ -442,7 +448,7 @@ def reverb_apply(x, spectrum, ir_length):
     ws = _workspace(_lib.query("reverb_workspace_size", B, T, int(ir_length)), x.device)
     _lib.call("reverb_apply", _lib.ptr(xc), _lib.ptr(spectrum), _lib.ptr(out), B, T, int(ir_length),
               _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
-    return out
+    return out, ws
 
 
 from . import grad as _grad  # noqa: E402  (autograd Functions over the backward kernels)

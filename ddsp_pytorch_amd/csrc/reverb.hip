@@ -153,27 +153,34 @@ int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, f
                      workspace, workspace_bytes, stream, true);
 }
 
-size_t ddsp_hip_reverb_ir_grad_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length) {
-  if (batch < 1 || n_samples < 1 || ir_length < 1) return 0;
-  return upols_corr_workspace_bytes(batch, n_samples, ir_length);
+size_t ddsp_hip_reverb_input_spectra_bytes(int64_t batch, int64_t n_samples) {
+  if (batch < 1 || n_samples < 1) return 0;
+  return upols_spectra_bytes(batch, n_samples);
 }
 
-int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impulse, int64_t batch,
-                            int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
-                            void* stream) {
-  if (batch < 0 || n_samples < 1 || ir_length < 1) return DDSP_HIP_EINVAL;
-  if (!grad_impulse) return DDSP_HIP_EINVAL;
+size_t ddsp_hip_reverb_backward_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length,
+                                               int have_input_spectra) {
+  if (batch < 1 || n_samples < 1 || ir_length < 1) return 0;
+  return upols_backward_workspace_bytes(batch, n_samples, ir_length, have_input_spectra != 0);
+}
+
+int ddsp_hip_reverb_backward(const float* x, const float* input_spectra, const float* spectrum, const float* grad,
+                             float* grad_x, float* grad_impulse, int64_t batch, int64_t n_samples,
+                             int64_t ir_length, void* workspace, size_t workspace_bytes, void* stream) {
+  if (batch < 0 || n_samples < 1 || ir_length < 1 || (!grad_x && !grad_impulse)) return DDSP_HIP_EINVAL;
   const int64_t kc = std::min(ir_length, n_samples);
-  if (kc < ir_length) {  // taps past the input length were cropped: zero gradient
+  if (grad_impulse && kc < ir_length) {  // taps past the input length were cropped: zero gradient
     hipError_t e = hipMemsetAsync(grad_impulse + kc, 0, sizeof(float) * (ir_length - kc), S(stream));
     if (e != hipSuccess) return DDSP_HIP_ELAUNCH;
   }
   if (batch == 0) {
+    if (!grad_impulse) return DDSP_HIP_OK;
     hipError_t e = hipMemsetAsync(grad_impulse, 0, sizeof(float) * kc, S(stream));
     return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;
   }
-  if (!x || !grad) return DDSP_HIP_EINVAL;
-  return upols_corr(x, grad, batch, n_samples, ir_length, grad_impulse, workspace, workspace_bytes, stream);
+  if (!grad || !spectrum || (grad_impulse && !x && !input_spectra)) return DDSP_HIP_EINVAL;
+  return upols_backward(x, input_spectra, spectrum, grad, batch, n_samples, ir_length, grad_x, grad_impulse,
+                        workspace, workspace_bytes, stream);
 }
 
 size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length) {

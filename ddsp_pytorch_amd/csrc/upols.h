@@ -21,9 +21,12 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
 int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
                 bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream,
                 bool reverse = false);
-// dimp[tau] = sum_rows sum_t g[row][t+tau] x[row][t], tau < min(klen, n) (kernel gradient of a
-// kernel shared by all rows); writes min(klen, n) values.
-size_t upols_corr_workspace_bytes(int64_t rows, int64_t n, int64_t klen);
-int upols_corr(const float* x, const float* g, int64_t rows, int64_t n, int64_t klen, float* dimp, void* ws,
-               size_t ws_bytes, void* stream);
+// bytes of the input spectra X that upols_apply leaves at the start of its workspace (pairing)
+size_t upols_spectra_bytes(int64_t rows, int64_t n);
+// Backward of upols_apply with a kernel shared by all rows (pairing): dx[rows, n] (nullable) and
+// dimp[tau] = sum_rows sum_t g[row][t+tau] x[row][t] for tau < min(klen, n) (nullable).  x_spectra:
+// the forward's X (nullable: recomputed from x when dimp is requested).
+size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x);
+int upols_backward(const float* x, const float* x_spectra, const float* spectrum, const float* g, int64_t rows,
+                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream);
 }  // namespace ddsp

@@ -156,12 +156,13 @@ __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& 
 }
 
 // X[pair][b][:] = FFT(z[(b+off)P, (b+off+2)P)); grid (nb, npairs).
-//   off = -1: the overlap-save input windows;  off = 0 with zero_hi: FFT([z_b, 0]) (the
-//   zero-padded blocks of the IR-gradient correlation);  reverse: z read time-reversed
-//   (z'[s] = z[T-1-s], the transposed convolution of the input gradient).
+//   off = -1: the overlap-save input windows; with zero_half = 1 the first half is zeroed:
+//   FFT([0, z_b]), the adjoint of the inverse transform's "keep the second half" (backward);
+//   zero_half = 2 zeroes the second half.  reverse: z read time-reversed (z'[s] = z[T-1-s],
+//   the transposed convolution of the input gradient).
 __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
                                                             int64_t T, int rows, int pairing, int nb,
-                                                            int off, int zero_hi, int reverse,
+                                                            int off, int zero_half, int reverse,
                                                             float2* __restrict__ X) {
   __shared__ float2 lds[kPad];
   const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t s = s0 + j + 256 * r;
-    const bool ok = s >= 0 && s < T && !(zero_hi && r >= 8);
+    const bool ok = s >= 0 && s < T && !(zero_half == 1 && r < 8) && !(zero_half == 2 && r >= 8);
     const int64_t si = reverse ? T - 1 - s : s;
     v[r] = make_float2(ok ? xa[si] : 0.0f, (ok && xb) ? xb[si] : 0.0f);
   }
@@ -275,13 +276,20 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
   }
 }
 
-// IR-gradient correlation (backward of Reverb.forward w.r.t. the impulse, modules.py:28-35):
-//   dH_p[f] = sum_{pair in group} sum_j conj(Xz[pair][j][f]) * Gw[pair][j+p][f]
-// with Xz_j = FFT([x_j, 0]) and Gw_k = FFT([g_k, g_{k+1}]): the circular correlation of the two
-// 2P windows is the exact linear correlation for lags pP + [0, P).  For a packed pair
-// (z = x_a + i x_b, same for g) the real part of the inverse transform is corr_a + corr_b, so
-// the packed spectra are used as they are.  One bin per thread, PC consecutive partitions with
-// a sliding register window of conj(Xz); grid (N/256, ceil(Q/PC), groups).
+// Backward of the partitioned convolution (Reverb.forward, modules.py:28-35), the adjoint of
+// each forward step (F = unnormalised FFT, its adjoint the unnormalised inverse):
+//   y_b = second half of F^-1(Y_b)           ->  dY_b = GZ_b = F([0, g_b])
+//   Y_b = sum_p X_{b-p} H_p                   ->  dX_j = sum_p conj(H_p) GZ_{j+p}   (upols_mac_adj_kernel)
+//                                                 dH_p = sum_b conj(X_{b-p}) GZ_b  (upols_corr_kernel)
+//   X_b = F([x_{b-1}, x_b])                   ->  dx_b = second half of F^-1(dX_b + (-1)^f dX_{b+1})
+//                                                 (the first half of F^-1(Z) is the second half of
+//                                                 F^-1((-1)^f Z)), so the forward's inverse kernel applies
+//   H_p = F([h_p, 0]) / N                     ->  dh_p = Re(first half of F^-1(dH_p)) / N
+// For a packed pair (z = x_a + i x_b, g likewise) the real part of F^-1(conj(X) GZ) is corr_a + corr_b:
+// the packed spectra are used as they are.  GZ is shared by both gradients, and X is the forward's.
+
+// dH_p[f] = sum_{pair in group} sum_j conj(X[pair][j][f]) * G[pair][j+p][f]: one bin per thread, PC
+// consecutive partitions with a sliding register window of conj(X); grid (N/256, ceil(Q/PC), groups).
 template <int PC>
 __global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restrict__ Xz,
                                                          const float2* __restrict__ Gw, int nb, int Q,
@@ -317,6 +325,48 @@ __global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restric
 #pragma unroll
   for (int d = 0; d < PC; ++d)
     if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = acc[d];
+}
+
+// T_j = sum_p conj(H_p) GZ_{j+p} for BLK+1 consecutive j, then V_j = T_j + (-1)^f T_{j+1} for the
+// BLK outputs (the inverse kernel's second half of F^-1(V_j) is dx_j).  grid (N/256, ceil(nb/BLK), npairs)
+template <int BLK>
+__global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __restrict__ G,
+                                                            const float2* __restrict__ Hs, int nb, int Q,
+                                                            float2* __restrict__ V) {
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int j0 = blockIdx.y * BLK;
+  const int pair = blockIdx.z;
+  const float2* Gp = G + (int64_t)pair * nb * kN + f;
+  const float2* Hp = Hs + f;
+  const float2 zero = make_float2(0.f, 0.f);
+  float2 acc[BLK + 1], win[BLK + 1];
+#pragma unroll
+  for (int d = 0; d <= BLK; ++d) {
+    acc[d] = zero;
+    const float2 gv = Gp[(int64_t)min(j0 + d, nb - 1) * kN];
+    win[d] = j0 + d < nb ? gv : zero;  // win[d] = GZ_{j0+d+p}
+  }
+  const int pmax = min(Q, nb - j0);
+#pragma unroll 4
+  for (int p = 0; p < pmax; ++p) {
+    const float2 h = Hp[(int64_t)p * kN];
+#pragma unroll
+    for (int d = 0; d <= BLK; ++d) {  // conj(h) * win
+      acc[d].x = fmaf(win[d].x, h.x, fmaf(win[d].y, h.y, acc[d].x));
+      acc[d].y = fmaf(win[d].y, h.x, fmaf(-win[d].x, h.y, acc[d].y));
+    }
+#pragma unroll
+    for (int d = 0; d < BLK; ++d) win[d] = win[d + 1];
+    const int kn = j0 + BLK + p + 1;
+    const float2 gv = Gp[(int64_t)min(kn, nb - 1) * kN];
+    win[BLK] = kn < nb ? gv : zero;
+  }
+  const float sgn = (f & 1) ? -1.0f : 1.0f;
+  float2* Vp = V + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int d = 0; d < BLK; ++d)
+    if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(fmaf(sgn, acc[d + 1].x, acc[d].x),
+                                                               fmaf(sgn, acc[d + 1].y, acc[d].y));
 }
 
 // dimp[pP + n] = Re(IFFT(sum_groups part[grp][p])) [n] / N for n < P, pP + n < klen; grid (Q)
@@ -396,40 +446,63 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   return launch_status();
 }
 
-size_t upols_corr_workspace_bytes(int64_t rows, int64_t n, int64_t klen) {
+size_t upols_spectra_bytes(int64_t rows, int64_t n) {
   const int64_t npairs = (rows + 1) / 2;
-  const int64_t nb = upols_blocks(n);
-  const int64_t Q = upols_partitions(std::min(klen, n));
-  const int64_t groups = std::min<int64_t>(npairs, 16);
-  return (2 * (size_t)npairs * nb + (size_t)groups * Q) * kN * sizeof(float2);
+  return (size_t)npairs * upols_blocks(n) * kN * sizeof(float2);
 }
 
-int upols_corr(const float* x, const float* g, int64_t rows, int64_t n, int64_t klen, float* dimp, void* ws,
-               size_t ws_bytes, void* stream) {
+size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x) {
+  const int64_t Q = upols_partitions(std::min(klen, n));
+  const int64_t groups = std::min<int64_t>((rows + 1) / 2, 16);
+  return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)groups * Q * kN * sizeof(float2);
+}
+
+int upols_backward(const float* x, const float* x_spectra, const float* spectrum, const float* g, int64_t rows,
+                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream) {
   const int64_t npairs = (rows + 1) / 2;
   const int64_t nb = upols_blocks(n);
   const int64_t kc = std::min(klen, n);
   const int64_t Q = upols_partitions(kc);
   const int64_t groups = std::min<int64_t>(npairs, 16);
   const int64_t ppg = (npairs + groups - 1) / groups;
-  if (!ws || ws_bytes < upols_corr_workspace_bytes(rows, n, klen)) return DDSP_HIP_EWORKSPACE;
-  if (nb > INT32_MAX || npairs > 65535 || Q > 65535) return DDSP_HIP_EINVAL;
-  float2* Xz = reinterpret_cast<float2*>(ws);
-  float2* Gw = Xz + (size_t)npairs * nb * kN;
-  float2* part = Gw + (size_t)npairs * nb * kN;
-  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     x, n, n, (int)rows, 1, (int)nb, 0, 1, 0, Xz);
+  const bool need_x = dimp && !x_spectra;
+  if (!ws || ws_bytes < upols_backward_workspace_bytes(rows, n, klen, !need_x)) return DDSP_HIP_EWORKSPACE;
+  if (nb > INT32_MAX || npairs > 65535 || Q > 65535 || (nb + 15) / 16 > 65535) return DDSP_HIP_EINVAL;
+  const size_t sb = upols_spectra_bytes(rows, n);
+  char* w = reinterpret_cast<char*>(ws);
+  float2* GZ = reinterpret_cast<float2*>(w);
+  float2* V = reinterpret_cast<float2*>(w + sb);
+  float2* part = reinterpret_cast<float2*>(w + 2 * sb);
+  float2* Xs = need_x ? reinterpret_cast<float2*>(w + 2 * sb + (size_t)groups * Q * kN * sizeof(float2))
+                      : const_cast<float2*>(reinterpret_cast<const float2*>(x_spectra));
+  // GZ_b = F([0, g_b])
+  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), g, n, n,
+                     (int)rows, 1, (int)nb, -1, 1, 0, GZ);
   int st = launch_status();
   if (st) return st;
-  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     g, n, n, (int)rows, 1, (int)nb, 0, 0, 0, Gw);
-  if ((st = launch_status())) return st;
-  hipLaunchKernelGGL(upols_corr_kernel<16>, dim3(kN / kNT, (unsigned)((Q + 15) / 16), (unsigned)groups),
-                     dim3(kNT), 0, S(stream), Xz, Gw, (int)nb, (int)Q, (int)npairs, (int)ppg, part);
-  if ((st = launch_status())) return st;
-  hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Q), dim3(kNT), 0, S(stream), part, (int)groups,
-                     (int)Q, kc, dimp);
-  return launch_status();
+  if (dx) {
+    hipLaunchKernelGGL(upols_mac_adj_kernel<16>, dim3(kN / kNT, (unsigned)((nb + 15) / 16), (unsigned)npairs),
+                       dim3(kNT), 0, S(stream), GZ, reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
+    if ((st = launch_status())) return st;
+    hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), V,
+                       (int)nb, n, (int)rows, 1, 0, dx, n);
+    if ((st = launch_status())) return st;
+  }
+  if (dimp) {
+    if (need_x) {
+      if (!x) return DDSP_HIP_EINVAL;
+      hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), x, n,
+                         n, (int)rows, 1, (int)nb, -1, 0, 0, Xs);
+      if ((st = launch_status())) return st;
+    }
+    hipLaunchKernelGGL(upols_corr_kernel<16>, dim3(kN / kNT, (unsigned)((Q + 15) / 16), (unsigned)groups),
+                       dim3(kNT), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)ppg, part);
+    if ((st = launch_status())) return st;
+    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Q), dim3(kNT), 0, S(stream), part, (int)groups,
+                       (int)Q, kc, dimp);
+    if ((st = launch_status())) return st;
+  }
+  return DDSP_HIP_OK;
 }
 
 }  // namespace ddsp

@@ -298,22 +298,16 @@ class SynthFramesFn(_F):
 
 
 # ------------------------------------------------------------------------------------------
-def reverb_transposed(g, spectrum, ir_length):
+def reverb_backward(x, x_spectra, spectrum, g, ir_length, want_dx, want_dimp):
+    """-> (dx or None, dimp or None) from one transform of g (csrc/upols.hip, upols_backward)."""
     B, T = g.shape[0], g.shape[1]
-    dx = torch.empty(B, T, 1, dtype=torch.float32, device=g.device)
-    ws = core._workspace(_lib.query("reverb_workspace_size", B, T, int(ir_length)), g.device)
-    _lib.call("reverb_apply_transposed", _lib.ptr(g), _lib.ptr(spectrum), _lib.ptr(dx), B, T, int(ir_length),
-              _lib.ptr(ws), ws.numel(), _lib.stream_of(g))
-    return dx
-
-
-def reverb_ir_grad(x, g, ir_length):
-    B, T = x.shape[0], x.shape[1]
-    dimp = torch.empty(int(ir_length), dtype=torch.float32, device=x.device)
-    ws = core._workspace(_lib.query("reverb_ir_grad_workspace_size", B, T, int(ir_length)), x.device)
-    _lib.call("reverb_ir_grad", _lib.ptr(x), _lib.ptr(g), _lib.ptr(dimp), B, T, int(ir_length), _lib.ptr(ws),
-              ws.numel(), _lib.stream_of(x))
-    return dimp
+    dx = torch.empty(B, T, 1, dtype=torch.float32, device=g.device) if want_dx else None
+    dimp = torch.empty(int(ir_length), dtype=torch.float32, device=g.device) if want_dimp else None
+    have = x_spectra is not None
+    ws = core._workspace(_lib.query("reverb_backward_workspace_size", B, T, int(ir_length), int(have)), g.device)
+    _lib.call("reverb_backward", _lib.ptr(x), _lib.ptr(x_spectra), _lib.ptr(spectrum), _lib.ptr(g), _lib.ptr(dx),
+              _lib.ptr(dimp), B, T, int(ir_length), _lib.ptr(ws), ws.numel(), _lib.stream_of(g))
+    return dx, dimp
 
 
 def impulse_backward(noise, decay, wet, dimp, grad_length, sample_rate):
@@ -339,30 +333,35 @@ class ReverbApplyFn(_F):
 
     @staticmethod
     def backward(ctx, g):
-        return reverb_transposed(_g(g), ctx.spectrum, ctx.L), None, None
+        dx, _ = reverb_backward(None, None, ctx.spectrum, _g(g), ctx.L, True, False)
+        return dx, None, None
 
 
 class ReverbFn(_F):
     """modules.py:21-35 Reverb.build_impulse + forward: gradients for the signal and for the
-    reverb's parameters (noise, decay, wet)."""
+    reverb's parameters (noise, decay, wet).  The forward's input spectra are kept for the
+    impulse gradient."""
 
     @staticmethod
     def forward(ctx, x, noise, decay, wet, spectrum, ir_length, sample_rate):
-        ctx.save_for_backward(x, noise, decay, wet)
+        out, ws = core._reverb_apply_launch(x, spectrum, ir_length)
+        ctx.save_for_backward(noise, decay, wet)
+        ctx.ws = ws if any(ctx.needs_input_grad[1:4]) else None
         ctx.spectrum = spectrum
+        ctx.T = x.shape[1]
         ctx.L, ctx.sr = int(ir_length), float(sample_rate)
-        return core.reverb_apply(x, spectrum, ir_length)
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        x, noise, decay, wet = ctx.saved_tensors
-        g = _g(g)
-        dx = reverb_transposed(g, ctx.spectrum, ctx.L) if ctx.needs_input_grad[0] else None
+        noise, decay, wet = ctx.saved_tensors
+        want_p = any(ctx.needs_input_grad[1:4])
+        dx, dimp = reverb_backward(None, ctx.ws, ctx.spectrum, _g(g), ctx.L, ctx.needs_input_grad[0], want_p)
         dn = dd = dw = None
-        if any(ctx.needs_input_grad[1:4]):
-            T = x.shape[1]
-            dimp = reverb_ir_grad(core._c(x.detach()), g, ctx.L)
-            dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), dimp, min(ctx.L, T), ctx.sr)
+        if want_p:
+            dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), dimp, min(ctx.L, ctx.T),
+                                          ctx.sr)
+        ctx.ws = None
         return dx, dn, dd, dw, None, None, None
 
 

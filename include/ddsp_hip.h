@@ -229,17 +229,22 @@ int ddsp_hip_filtered_noise_backward(const float* magnitudes, const float* noise
 /* modules.py:28-35 Reverb.forward backward.
  *   ddsp_hip_reverb_apply_transposed: grad_x[b,t] = sum_tau grad[b,t+tau] IR[tau] (same spectrum and
  *     workspace as ddsp_hip_reverb_apply);
- *   ddsp_hip_reverb_ir_grad: grad_impulse[tau] = sum_b sum_t grad[b,t+tau] x[b,t] for tau < L
- *     (zero for taps cropped away when L > n_samples);
+ *   ddsp_hip_reverb_backward: grad_x (nullable) as above and grad_impulse[tau] (nullable) =
+ *     sum_b sum_t grad[b,t+tau] x[b,t] for tau < L (zero for taps cropped away when L > n_samples),
+ *     sharing one transform of grad.  input_spectra (nullable): the first
+ *     ddsp_hip_reverb_input_spectra_bytes bytes of the workspace ddsp_hip_reverb_apply used for this
+ *     x, which hold x's partition spectra on return — kept by the caller, they spare a transform of x;
  *   ddsp_hip_reverb_impulse_backward (modules.py:21-26): grad_impulse -> grad_noise[L], and the
  *     device scalars grad_decay, grad_wet (taps >= grad_length carry no gradient). */
 int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, float* grad_x, int64_t batch,
                                      int64_t n_samples, int64_t ir_length, void* workspace,
                                      size_t workspace_bytes, void* stream);
-size_t ddsp_hip_reverb_ir_grad_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length);
-int ddsp_hip_reverb_ir_grad(const float* x, const float* grad, float* grad_impulse, int64_t batch,
-                            int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
-                            void* stream);
+size_t ddsp_hip_reverb_input_spectra_bytes(int64_t batch, int64_t n_samples);
+size_t ddsp_hip_reverb_backward_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length,
+                                               int have_input_spectra);
+int ddsp_hip_reverb_backward(const float* x, const float* input_spectra, const float* spectrum, const float* grad,
+                             float* grad_x, float* grad_impulse, int64_t batch, int64_t n_samples,
+                             int64_t ir_length, void* workspace, size_t workspace_bytes, void* stream);
 size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length);
 int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
                                      const float* grad_impulse, int64_t length, int64_t grad_length,

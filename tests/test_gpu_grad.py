@@ -278,3 +278,36 @@ def test_decoder_grad_golden(dd):
             assert relerr(p.grad, g[key]) < tol, (name, relerr(p.grad, g[key]))
             checked += 1
     assert checked >= 20
+
+
+def test_reverb_backward_entry_points(dd):
+    """The C-ABI's three ways to the reverb gradients agree: ddsp_hip_reverb_backward with the
+    forward's kept input spectra (the autograd path), the same entry recomputing them from x, and
+    ddsp_hip_reverb_apply_transposed for the input gradient."""
+    from ddsp_pytorch_amd import _lib, core, grad
+    g_ = torch.Generator().manual_seed(21)
+    B, T, L = 5, 20000, 9000
+    x = (torch.randn(B, T, 1, generator=g_) * 0.3).cuda()
+    w = torch.randn(B, T, 1, generator=g_).cuda()
+    torch.manual_seed(1)
+    rv = dd.modules.Reverb(L, 48000).cuda()
+    with torch.no_grad():
+        spec = core.reverb_spectrum(rv.build_impulse(), T)
+        _, ws = core._reverb_apply_launch(x, spec, L)
+    dx1, di1 = grad.reverb_backward(None, ws, spec, w, L, True, True)
+    dx2, di2 = grad.reverb_backward(x, None, spec, w, L, True, True)
+    assert torch.equal(dx1, dx2) and torch.equal(di1, di2)
+    dx3 = torch.empty_like(dx1)
+    ws3 = core._workspace(_lib.query("reverb_workspace_size", B, T, L), x.device)
+    _lib.call("reverb_apply_transposed", _lib.ptr(w), _lib.ptr(spec), _lib.ptr(dx3), B, T, L, _lib.ptr(ws3),
+              ws3.numel(), _lib.stream_of(w))
+    assert relerr(dx3, dx1) < 1e-6
+    # against the oracle
+    noise, decay, wet = (p.detach().cpu().clone() for p in (rv.noise, rv.decay, rv.wet))
+    imp = tr.Reverb(noise, decay, wet, L, 48000).build_impulse().reshape(-1)
+    xc = x.cpu().requires_grad_(True)
+    ic = imp.clone().requires_grad_(True)
+    y = tr.fft_convolve(xc.squeeze(-1), torch.nn.functional.pad(ic, (0, T - L)))
+    (y * w.cpu().squeeze(-1)).sum().backward()
+    assert relerr(dx1, xc.grad) < GRAD_REL
+    assert relerr(di1, ic.grad) < GRAD_REL
