@@ -4,8 +4,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 SRC := ddsp_pytorch_amd/csrc/synth.hip ddsp_pytorch_amd/csrc/noise.hip ddsp_pytorch_amd/csrc/reverb.hip \
        ddsp_pytorch_amd/csrc/upols.hip ddsp_pytorch_amd/csrc/synth_frame.hip \
-       ddsp_pytorch_amd/csrc/backward.hip
-HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h ddsp_pytorch_amd/csrc/upols.h \
+       ddsp_pytorch_amd/csrc/backward.hip ddsp_pytorch_amd/csrc/stft.hip
+HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h ddsp_pytorch_amd/csrc/upols.h ddsp_pytorch_amd/csrc/fft_radix.h \
        ddsp_pytorch_amd/csrc/noise_dsp.h
 LIB := ddsp_pytorch_amd/lib/libddsp_hip.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ibuild -Wall -Wno-unused-result
@@ -26,7 +26,7 @@ build/twiddle4096.inc: tools/gen_twiddles.py
 	@mkdir -p build
 	python3 tools/gen_twiddles.py 4096 > $@
 
-build/upols.o build/noise.o build/synth_frame.o build/backward.o: build/twiddle4096.inc
+build/upols.o build/noise.o build/synth_frame.o build/backward.o build/stft.o: build/twiddle4096.inc
 
 build/%.o: ddsp_pytorch_amd/csrc/%.hip $(HDR)
 	@mkdir -p build

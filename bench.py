@@ -62,6 +62,8 @@ def parse():
                         "'gathered'; value is always the left-sharded throughput)")
     p.add_argument("--no-train-leg", action="store_true",
                    help="skip the training-step leg (synthesis forward + backward kernels)")
+    p.add_argument("--no-loss-leg", action="store_true",
+                   help="skip the multiscale spectral loss leg (forward + backward, both signals)")
     p.add_argument("--no-decoder-leg", action="store_true",
                    help="skip the full DDSPDecoder.forward leg (GRU/MLP + synthesis)")
     p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
@@ -193,6 +195,58 @@ def train_leg(args, inp, dev, reps=20):
     return {"value": round(B * F * bs / t, 1), "unit": "samples/s", "ms_per_step": round(t * 1e3, 4),
             "event_ms": ms, "gradients": "param [B,F,H+1], mags [B,F,NB], reverb noise/decay/wet",
             "workload": f"config {args.config} synthesis forward + backward, batch {B}/GPU"}
+
+
+def loss_leg(args, dev, reps=10):
+    """train.py:91-104's multiscale spectral loss (scales 4096..128, 75%
+    overlap) of a target and a reconstruction [B, T], forward + backward w.r.t. the
+    reconstruction — on the gfx950 STFT kernels, and on torch.stft (rocFFT) for comparison."""
+    from ddsp_pytorch_amd import core
+    from ddsp_pytorch_amd.loss import multiscale_spec_loss
+    B, T = args.batch, args.frames * args.block_size
+    scales = (4096, 2048, 1024, 512, 256, 128)
+    g = torch.Generator(device=dev).manual_seed(5)
+    sig = torch.randn(B, T, device=dev, generator=g) * 0.3
+    rec = (sig + 0.05 * torch.randn(B, T, device=dev, generator=g)).requires_grad_(True)
+
+    def torch_fft(x):
+        return [torch.stft(x, s, s // 4, s, torch.hann_window(s, device=dev), True, normalized=True,
+                           return_complex=True).abs() for s in scales]
+
+    def run(fn):
+        for _ in range(3):
+            rec.grad = None
+            multiscale_spec_loss(fn(sig), fn(rec)).backward()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rec.grad = None
+            multiscale_spec_loss(fn(sig), fn(rec)).backward()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    def run_fused():
+        from ddsp_pytorch_amd.loss import spectral_loss
+        for _ in range(3):
+            rec.grad = None
+            spectral_loss(sig, rec, scales, 0.75).backward()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rec.grad = None
+            spectral_loss(sig, rec, scales, 0.75).backward()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    t_fused = run_fused()
+    t_ours = run(lambda x: core.multiscale_fft(x, scales, 0.75))
+    t_torch = run(torch_fft)
+    return {"value": round(B * T / t_fused, 1), "unit": "samples/s", "ms_per_step": round(t_fused * 1e3, 4),
+            "spectrogram_route_ms_per_step": round(t_ours * 1e3, 4),
+            "torch_stft_ms_per_step": round(t_torch * 1e3, 4),
+            "workload": f"multiscale spectral loss fwd+bwd, batch {B} x {T} samples, scales {list(scales)}; "
+                        "value: fused ddsp_hip_spectral_loss; spectrogram route: core.multiscale_fft + "
+                        "train.py's loss in torch; torch_stft: the reference's torch.stft (rocFFT) on the GPU"}
 
 
 def decoder_leg(args, inp, dev, reps=10):
@@ -363,6 +417,9 @@ def main():
 
     if rank == 0 and not args.no_train_leg:
         result["train_step"] = train_leg(args, inp, dev)
+
+    if rank == 0 and not args.no_loss_leg:
+        result["spectral_loss"] = loss_leg(args, dev)
 
     if rank == 0 and not args.no_decoder_leg:
         result["decoder_forward"] = decoder_leg(args, inp, dev)

@@ -46,6 +46,13 @@ SIGNATURES = {
     "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
     "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P]),
     "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    # multiscale STFT (training loss)
+    "ddsp_hip_stft_frames": (_I64, [_I64, _I64]),
+    "ddsp_hip_stft_magnitude": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),
+    "ddsp_hip_stft_backward_workspace_size": (_SZ, [_I64, _I64, _I64, _I64]),
+    "ddsp_hip_stft_magnitude_backward": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_spectral_loss_workspace_size": (_SZ, [_I64, _I64, _P, _P, _I]),
+    "ddsp_hip_spectral_loss": (_I, [_P, _P, _I64, _I64, _P, _P, _I, _P, _P, _P, _SZ, _P]),
     # backward
     "ddsp_hip_scale_function_backward": (_I, [_P, _P, _P, _I64, _F, _P]),
     "ddsp_hip_upsample_backward": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),

@@ -24,7 +24,7 @@ __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
     "harmonic_synth_frames", "harmonic_synth_params", "synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
-    "reverb_spectrum", "reverb_apply", "set_noise_seed",
+    "reverb_spectrum", "reverb_apply", "set_noise_seed", "safe_log", "stft_magnitude", "multiscale_fft",
 ]
 
 
@@ -435,6 +435,36 @@ def reverb_apply(x, spectrum, ir_length):
                                       "modules.Reverb (gradients for noise/decay/wet) instead")
         return _grad.ReverbApplyFn.apply(x, spectrum, int(ir_length))
     return _reverb_apply_launch(x, spectrum, ir_length)[0]
+
+
+# ------------------------------------------------------------------------------------
+# training loss (ddsp/core.py:10-41; train.py:70-76)
+# ------------------------------------------------------------------------------------
+def safe_log(x):
+    """ddsp/core.py:10-11."""
+    return torch.log(x + 1e-7)
+
+
+def stft_magnitude(signal, n_fft, hop):
+    """|torch.stft(signal, n_fft, hop, n_fft, hann_window(n_fft), center=True, normalized=True)|
+    for signal [B, T] -> [B, n_fft/2+1, frames] (a transposed view of the kernel's frame-major
+    output; the values and shape are the reference's)."""
+    _dev(signal)
+    if signal.dim() != 2:
+        raise RuntimeError(f"stft_magnitude: expected [batch, time], got {tuple(signal.shape)}")
+    if _wants_grad(signal):
+        return _grad.StftMagFn.apply(signal, int(n_fft), int(hop))
+    B, T = signal.shape
+    x = _c(signal)
+    frames = int(_lib.query("stft_frames", T, int(hop)))
+    M = torch.empty(B, frames, int(n_fft) // 2 + 1, dtype=torch.float32, device=x.device)
+    _lib.call("stft_magnitude", _lib.ptr(x), _lib.ptr(M), B, T, int(n_fft), int(hop), _lib.stream_of(x))
+    return M.transpose(1, 2)
+
+
+def multiscale_fft(signal, scales, overlap):
+    """ddsp/core.py:27-41: one magnitude spectrogram per scale, hop int(s * (1 - overlap))."""
+    return [stft_magnitude(signal, s, int(s * (1 - overlap))) for s in scales]
 
 
 def _reverb_apply_launch(x, spectrum, ir_length):

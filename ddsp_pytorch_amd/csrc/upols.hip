@@ -23,100 +23,13 @@
 
 #include "common.h"
 #include "upols.h"
-#include "twiddle4096.inc"
+#include "fft_radix.h"
 
 namespace ddsp {
 namespace {
 
 constexpr int kNT = 256;            // threads per transform
 constexpr int kPad = kN + kN / 16;  // LDS float2 slots: one pad slot per 16 (bank spreading)
-
-__device__ __forceinline__ int lds_idx(int i) { return i + (i >> 4); }
-
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
-}
-
-__device__ __forceinline__ float2 twiddle(int m, bool inv) {
-  const float2 w = reinterpret_cast<const float2*>(kTwiddle4096)[m];
-  return inv ? make_float2(w.x, -w.y) : w;
-}
-
-template <bool INV>
-__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
-  const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
-  const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
-  const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
-  const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
-  // forward: W4 = -i ; inverse: +i.  (-i)*(x+iy) = y - ix
-  const float2 rot = INV ? make_float2(-d13.y, d13.x) : make_float2(d13.y, -d13.x);
-  a0 = make_float2(s02.x + s13.x, s02.y + s13.y);
-  a2 = make_float2(s02.x - s13.x, s02.y - s13.y);
-  a1 = make_float2(d02.x + rot.x, d02.y + rot.y);
-  a3 = make_float2(d02.x - rot.x, d02.y - rot.y);
-}
-
-// 16-point DFT in registers: r = 4 r1 + r0, k = k0 + 4 k1.
-template <bool INV>
-__device__ __forceinline__ void dft16(float2 (&v)[16]) {
-#pragma unroll
-  for (int r0 = 0; r0 < 4; ++r0) dft4<INV>(v[r0], v[4 + r0], v[8 + r0], v[12 + r0]);
-  // v[4*k0 + r0] now holds u[r0][k0]; internal twiddles W16^{r0*k0} = W4096^{256*r0*k0}
-#pragma unroll
-  for (int r0 = 1; r0 < 4; ++r0)
-#pragma unroll
-    for (int k0 = 1; k0 < 4; ++k0) v[4 * k0 + r0] = cmul(v[4 * k0 + r0], twiddle(256 * r0 * k0, INV));
-  float2 t[16];
-#pragma unroll
-  for (int k0 = 0; k0 < 4; ++k0) {
-    float2 a0 = v[4 * k0 + 0], a1 = v[4 * k0 + 1], a2 = v[4 * k0 + 2], a3 = v[4 * k0 + 3];
-    dft4<INV>(a0, a1, a2, a3);
-    t[k0 + 0] = a0; t[k0 + 4] = a1; t[k0 + 8] = a2; t[k0 + 12] = a3;  // X[k0 + 4 k1]
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = t[i];
-}
-
-// Twiddles w^r, r = 1..15, of one Stockham pass from four table loads (w, w^2, w^4, w^8):
-// every other power is a product of at most three table values (error <= ~3 ulp), so a pass
-// costs 4 global loads instead of 15 and they can be issued before the LDS phases.
-struct Tw4 {
-  float2 t1, t2, t4, t8;
-};
-
-template <bool INV>
-__device__ __forceinline__ Tw4 load_tw(int step) {
-  Tw4 t;
-  t.t1 = twiddle(step, INV);
-  t.t2 = twiddle(2 * step, INV);
-  t.t4 = twiddle(4 * step, INV);
-  t.t8 = twiddle(8 * step, INV);
-  return t;
-}
-
-__device__ __forceinline__ void apply_tw(float2 (&v)[16], const Tw4& t) {
-  const float2 w3 = cmul(t.t1, t.t2), w5 = cmul(t.t4, t.t1), w6 = cmul(t.t4, t.t2);
-  const float2 w7 = cmul(t.t4, w3);
-  v[1] = cmul(v[1], t.t1);
-  v[2] = cmul(v[2], t.t2);
-  v[3] = cmul(v[3], w3);
-  v[4] = cmul(v[4], t.t4);
-  v[5] = cmul(v[5], w5);
-  v[6] = cmul(v[6], w6);
-  v[7] = cmul(v[7], w7);
-  v[8] = cmul(v[8], t.t8);
-  v[9] = cmul(v[9], cmul(t.t8, t.t1));
-  v[10] = cmul(v[10], cmul(t.t8, t.t2));
-  v[11] = cmul(v[11], cmul(t.t8, w3));
-  v[12] = cmul(v[12], cmul(t.t8, t.t4));
-  v[13] = cmul(v[13], cmul(t.t8, w5));
-  v[14] = cmul(v[14], cmul(t.t8, w6));
-  v[15] = cmul(v[15], cmul(t.t8, w7));
-}
-
-__device__ __forceinline__ int out_index(int j, int Ns, int r) {
-  return (j / Ns) * Ns * 16 + (j & (Ns - 1)) + r * Ns;
-}
 
 // Full 4096-point transform (three radix-16 Stockham passes, Ns = 1, 16, 256):
 // v holds in[j + 256 r] on entry and out[j + 256 r] on exit.

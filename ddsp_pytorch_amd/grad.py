@@ -380,3 +380,26 @@ class BuildImpulseFn(_F):
         g = _g(g).reshape(-1)
         dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), g, noise.shape[0], ctx.sr)
         return dn, dd, dw, None
+
+
+# ------------------------------------------------------------------------------------------
+class StftMagFn(_F):
+    """ddsp/core.py:27-41 (one scale): |STFT| of signal [B, T]; backward through the magnitude,
+    the transform, the window and the reflect padding (csrc/stft.hip)."""
+
+    @staticmethod
+    def forward(ctx, signal, n_fft, hop):
+        ctx.save_for_backward(signal)
+        ctx.n_fft, ctx.hop = n_fft, hop
+        return core.stft_magnitude(signal, n_fft, hop)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        B, T = x.shape
+        gM = core._c(g.transpose(1, 2))  # frame-major, the kernel's layout
+        dx = torch.empty(B, T, dtype=torch.float32, device=x.device)
+        ws = core._workspace(_lib.query("stft_backward_workspace_size", B, T, ctx.n_fft, ctx.hop), x.device)
+        _lib.call("stft_magnitude_backward", _lib.ptr(core._c(x.detach())), _lib.ptr(gM), _lib.ptr(dx), B, T,
+                  ctx.n_fft, ctx.hop, _lib.ptr(ws), ws.numel(), _lib.stream_of(dx))
+        return dx, None, None

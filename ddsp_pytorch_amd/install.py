@@ -10,6 +10,9 @@ from . import core, modules
 
 FUNCTIONS = ("scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
              "amp_to_impulse_response", "fft_convolve")
+# the training loss's spectrograms (core.py:27-41); train.py:9 binds them at import time, so
+# install() must run before train.py is imported.  Rebound on ddsp and ddsp.core.
+LOSS_FUNCTIONS = ("multiscale_fft", "safe_log")
 METHODS = {
     "HarmonicSynth": ("get_controls", "forward"),
     "FilteredNoise": ("get_controls", "forward", "draw_noise"),
@@ -22,8 +25,8 @@ class Installation:
         self.pkg, self._fns, self._methods = pkg, saved_fns, saved_methods
 
     def uninstall(self):
-        for name, fn in self._fns.items():
-            setattr(self.pkg, name, fn)
+        for (obj, name), fn in self._fns.items():
+            setattr(obj, name, fn)
         for (cls, name), fn in self._methods.items():
             if fn is None:
                 delattr(cls, name)
@@ -45,8 +48,13 @@ def install(pkg=None, functions=True, module_forwards=True):
     saved_fns, saved_methods = {}, {}
     if functions:
         for name in FUNCTIONS:
-            saved_fns[name] = getattr(pkg, name)
+            saved_fns[(pkg, name)] = getattr(pkg, name)
             setattr(pkg, name, getattr(core, name))
+        for obj in (pkg, getattr(pkg, "core", None)):
+            for name in LOSS_FUNCTIONS:
+                if obj is not None and hasattr(obj, name):
+                    saved_fns[(obj, name)] = getattr(obj, name)
+                    setattr(obj, name, getattr(core, name))
     if module_forwards:
         ref_modules = pkg.models.modules
         for cls_name, names in METHODS.items():

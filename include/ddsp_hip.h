@@ -159,6 +159,32 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* ---------------- training loss: ddsp/core.py:27-41 multiscale_fft ----------------
+ * One scale of multiscale_fft: |torch.stft(x, n_fft, hop, n_fft, hann(n_fft), center=True
+ * (reflect), normalized=True)| for x[batch, n_samples] (n_fft a power of two in [16, 4096],
+ * n_samples > n_fft/2).  magnitudes are written frame-major [batch, frames, n_fft/2+1]
+ * (frames = ddsp_hip_stft_frames(n_samples, hop) = n_samples/hop + 1); the reference's
+ * [batch, n_fft/2+1, frames] is its transpose.  The backward maps grad_magnitudes (same layout)
+ * to grad_x[batch, n_samples] (|Z| has zero gradient where Z = 0, as torch's abs). */
+int64_t ddsp_hip_stft_frames(int64_t n_samples, int64_t hop);
+int ddsp_hip_stft_magnitude(const float* x, float* magnitudes, int64_t batch, int64_t n_samples, int64_t n_fft,
+                            int64_t hop, void* stream);
+size_t ddsp_hip_stft_backward_workspace_size(int64_t batch, int64_t n_samples, int64_t n_fft, int64_t hop);
+int ddsp_hip_stft_magnitude_backward(const float* x, const float* grad_magnitudes, float* grad_x, int64_t batch,
+                                     int64_t n_samples, int64_t n_fft, int64_t hop, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+
+/* train.py:70-76 + 91-104: the multiscale spectral loss of a reconstruction against a target
+ * (both [batch, n_samples]), sum over scales of mean|Mx - My| + mean|log(Mx+1e-7) - log(My+1e-7)|,
+ * fused per scale (no spectrogram reaches memory) -> loss (device scalar) and, when grad_recon is
+ * not NULL, dloss/drecon [batch, n_samples].  n_ffts/hops: host arrays of n_scales entries
+ * (hop = int(n_fft * (1 - overlap))).  Deterministic (fixed-order fp64 reductions). */
+size_t ddsp_hip_spectral_loss_workspace_size(int64_t batch, int64_t n_samples, const int64_t* n_ffts,
+                                             const int64_t* hops, int n_scales);
+int ddsp_hip_spectral_loss(const float* target, const float* recon, int64_t batch, int64_t n_samples,
+                           const int64_t* n_ffts, const int64_t* hops, int n_scales, float* loss, float* grad_recon,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------- backward (training): train.py:84-130 back-propagates through the path ----------------
  * Vector-Jacobian products of the entry points above.  `grad*` inputs are the upstream
  * gradients (same shapes as the forward outputs), `grad_*` outputs are caller-allocated and

@@ -113,3 +113,26 @@ def synth_path_autograd(f0, param, mags, noise, reverb, block_size, sample_rate)
 
 synth_path = torch.no_grad()(synth_path_autograd)
 synth_path.__doc__ = "synth_path_autograd under torch.no_grad() (the CPU baseline's forward)."
+
+
+def safe_log(x):
+    # ddsp/core.py:10-11
+    return torch.log(x + 1e-7)
+
+
+def multiscale_fft(signal, scales, overlap):
+    # ddsp/core.py:27-41
+    out = []
+    for s in scales:
+        S = torch.stft(signal, s, int(s * (1 - overlap)), s, torch.hann_window(s).to(signal), True,
+                       normalized=True, return_complex=True).abs()
+        out.append(S)
+    return out
+
+
+def multiscale_spec_loss(ori_stft, rec_stft):
+    # train.py:70-76
+    loss = 0
+    for s_x, s_y in zip(ori_stft, rec_stft):
+        loss = loss + (s_x - s_y).abs().mean() + (safe_log(s_x) - safe_log(s_y)).abs().mean()
+    return loss

@@ -191,11 +191,11 @@ def main():
          distribution=o["harmonic_ctrls"]["harmonic_distribution"],
          magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
 
-    grad_goldens(decoder, modules, sr)
+    grad_goldens(ddsp, decoder, modules, sr)
 
 
 @torch.enable_grad()
-def grad_goldens(decoder, modules, sr):
+def grad_goldens(ddsp, decoder, modules, sr):
     # ---------------- g6: gradients (train.py:84-130 back-propagates through the path) ----------------
     # loss = sum(signal * w) with a fixed random w, so d loss / d signal = w exactly.
     torch.manual_seed(0)
@@ -233,6 +233,20 @@ def grad_goldens(decoder, modules, sr):
         save(f"g6_grad_reverb_{tag}", length=L, sample_rate=sr, noise=rv.noise.detach(), decay=rv.decay.detach(),
              wet=rv.wet.detach(), x=x.detach(), weight=w, out=out.detach(), grad_x=x.grad,
              grad_noise=rv.noise.grad, grad_decay=rv.decay.grad, grad_wet=rv.wet.grad)
+
+    # ---------------- g7: the training loss (core.py:27-41 multiscale_fft, train.py:70-76) ----------------
+    g = torch.Generator().manual_seed(17)
+    sig = torch.randn(2, 8192, generator=g) * 0.3
+    rec = (sig + 0.1 * torch.randn(2, 8192, generator=g)).requires_grad_(True)
+    scales, overlap = [4096, 2048, 1024, 512, 256, 128], 0.75
+    ori_stft = ddsp.core.multiscale_fft(sig, scales, overlap)
+    rec_stft = ddsp.core.multiscale_fft(rec, scales, overlap)
+    loss = 0
+    for s_x, s_y in zip(ori_stft, rec_stft):  # train.py:70-76
+        loss = loss + (s_x - s_y).abs().mean() + (ddsp.core.safe_log(s_x) - ddsp.core.safe_log(s_y)).abs().mean()
+    loss.backward()
+    save("g7_stft_loss", sig=sig, rec=rec.detach(), scales=np.array(scales), overlap=overlap, loss=loss.detach(),
+         grad_rec=rec.grad, **{f"stft_{s}": m.detach() for s, m in zip(scales, rec_stft)})
 
 
 if __name__ == "__main__":

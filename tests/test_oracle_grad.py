@@ -53,3 +53,18 @@ def test_decoder_synth_grad():
     assert relerr(mags.grad, g["grad_mags"]) < 1e-6, relerr(mags.grad, g["grad_mags"])
     for k, t in (("noise", noise), ("decay", decay), ("wet", wet)):
         assert relerr(t.grad, g["grad.reverb." + k]) < 1e-6, (k, relerr(t.grad, g["grad.reverb." + k]))
+
+
+def test_stft_loss_oracle():
+    """The oracle's multiscale STFT loss and its gradient reproduce the reference's (g7)."""
+    g = load_golden("g7_stft_loss")
+    scales, overlap = [int(s) for s in g["scales"]], float(g["overlap"])
+    rec = T(g["rec"]).clone().requires_grad_(True)
+    ori = tr.multiscale_fft(T(g["sig"]), scales, overlap)
+    rs = tr.multiscale_fft(rec, scales, overlap)
+    for s, m in zip(scales, rs):
+        assert torch.equal(m.detach(), T(g[f"stft_{s}"]))
+    loss = tr.multiscale_spec_loss(ori, rs)
+    assert torch.equal(loss.detach(), T(g["loss"]))
+    loss.backward()
+    assert relerr(rec.grad, g["grad_rec"]) < 1e-6
