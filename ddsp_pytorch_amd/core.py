@@ -438,6 +438,37 @@ def reverb_apply(x, spectrum, ir_length):
 
 
 # ------------------------------------------------------------------------------------
+# the decoder network's recurrence (decoder.py:33-68)
+# ------------------------------------------------------------------------------------
+def gru_supported(gru_module):
+    """Shapes the step kernel takes: one layer, batch_first, unidirectional, biased, hidden % 64 == 0."""
+    g = gru_module
+    return (g.num_layers == 1 and g.batch_first and not g.bidirectional and g.bias and
+            g.hidden_size % 64 == 0 and g.hidden_size <= 4096)
+
+
+def gru(x, gru_module, h0=None):
+    """torch.nn.GRU(x, h0) forward (1 layer, batch_first) -> (out [B,T,H], h_T [1,B,H]): the input
+    projection for all steps as one GEMM, the recurrence on the gfx950 step kernel.  Inference
+    only (callers keep torch's GRU where autograd needs its backward)."""
+    _dev(x)
+    if not gru_supported(gru_module):
+        raise RuntimeError("gru: one layer, batch_first, unidirectional, with bias and hidden % 64 == 0 expected")
+    B, T, _ = x.shape
+    H = gru_module.hidden_size
+    w_ih, w_hh = gru_module.weight_ih_l0, gru_module.weight_hh_l0
+    b_ih, b_hh = gru_module.bias_ih_l0, gru_module.bias_hh_l0
+    with torch.no_grad():
+        xp = torch.addmm(b_ih, x.reshape(B * T, -1), w_ih.t()).view(B, T, 3 * H)
+        out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
+        h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
+        h0c = _c(h0.reshape(B, H)) if h0 is not None else None
+        _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
+                  _lib.ptr(h_last), B, T, H, _lib.stream_of(out))
+    return out, h_last
+
+
+# ------------------------------------------------------------------------------------
 # training loss (ddsp/core.py:10-41; train.py:70-76)
 # ------------------------------------------------------------------------------------
 def safe_log(x):

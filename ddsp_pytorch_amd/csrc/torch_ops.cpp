@@ -267,6 +267,31 @@ at::Tensor reverb_apply(const at::Tensor& x, const at::Tensor& spectrum, int64_t
 
 }  // namespace
 
+// ---------------- decoder.py:33-68: the GRU recurrence ----------------
+std::tuple<at::Tensor, at::Tensor> gru(const at::Tensor& x, const at::Tensor& w_ih, const at::Tensor& w_hh,
+                                       const at::Tensor& b_ih, const at::Tensor& b_hh,
+                                       const std::optional<at::Tensor>& h0) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 3, "gru: x must be [batch, time, features]");
+  const int64_t B = x.size(0), T = x.size(1), H = w_hh.size(1);
+  TORCH_CHECK(w_hh.size(0) == 3 * H && w_ih.size(0) == 3 * H && w_ih.size(1) == x.size(2), "gru: weight shapes");
+  at::Tensor xp = at::addmm(b_ih, x.reshape({B * T, x.size(2)}), w_ih.t()).view({B, T, 3 * H});
+  at::Tensor out = at::empty({B, T, H}, x.options());
+  at::Tensor h_last = at::empty({1, B, H}, x.options());
+  at::Tensor h0c;
+  if (h0.has_value() && h0->defined()) {
+    check_dev(*h0, "h0");
+    TORCH_CHECK(h0->numel() == B * H, "gru: h0 must hold batch x hidden values");
+    h0c = c16(h0->reshape({B, H}));
+  }
+  at::Tensor whh = c16(w_hh), bhh = c16(b_hh);
+  ok(ddsp_hip_gru_forward(xp.data_ptr<float>(), whh.data_ptr<float>(), bhh.data_ptr<float>(),
+                          h0c.defined() ? h0c.data_ptr<float>() : nullptr, out.data_ptr<float>(),
+                          h_last.data_ptr<float>(), B, T, H, stream_of(x)),
+     "gru_forward");
+  return {out, h_last};
+}
+
 TORCH_LIBRARY(ddsp_hip, m) {
   m.def("scale_function(Tensor x) -> Tensor");
   m.def("remove_above_nyquist(Tensor amplitudes, Tensor f0, float sample_rate) -> Tensor");
@@ -284,6 +309,7 @@ TORCH_LIBRARY(ddsp_hip, m) {
   m.def("reverb_build_impulse(Tensor noise, Tensor decay, Tensor wet, float sample_rate) -> Tensor");
   m.def("reverb_spectrum(Tensor impulse, int n_samples) -> Tensor");
   m.def("reverb_apply(Tensor x, Tensor spectrum, int ir_length) -> Tensor");
+  m.def("gru(Tensor x, Tensor w_ih, Tensor w_hh, Tensor b_ih, Tensor b_hh, Tensor? h0=None) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ddsp_hip, CUDA, m) {  // HIP tensors dispatch under the CUDA key on ROCm
@@ -300,4 +326,5 @@ TORCH_LIBRARY_IMPL(ddsp_hip, CUDA, m) {  // HIP tensors dispatch under the CUDA 
   m.impl("reverb_build_impulse", &reverb_build_impulse);
   m.impl("reverb_spectrum", &reverb_spectrum);
   m.impl("reverb_apply", &reverb_apply);
+  m.impl("gru", &gru);
 }

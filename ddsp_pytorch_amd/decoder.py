@@ -11,6 +11,7 @@ reference calls it.
 import torch
 import torch.nn as nn
 
+from . import core
 from .modules import FilteredNoise, HarmonicSynth, Reverb
 
 
@@ -36,11 +37,18 @@ class GRUDecoder(nn.Module):
 
     def forward(self, f0, loudness, realtime: bool = False):
         hidden = torch.cat([self.f0_mlp(f0), self.loudness_mlp(loudness)], -1)
+        # the recurrence on the gfx950 step kernel for inference; torch's GRU (MIOpen) when
+        # autograd needs its backward
+        native = hidden.is_cuda and core.gru_supported(self.gru) and not (
+            torch.is_grad_enabled() and (hidden.requires_grad or self.gru.weight_hh_l0.requires_grad))
         if realtime:
-            gru_out, cache = self.gru(hidden, self.cache_gru)
+            if native:
+                gru_out, cache = core.gru(hidden, self.gru, self.cache_gru)
+            else:
+                gru_out, cache = self.gru(hidden, self.cache_gru)
             self.cache_gru.copy_(cache)
         else:
-            gru_out = self.gru(hidden)[0]
+            gru_out = core.gru(hidden, self.gru)[0] if native else self.gru(hidden)[0]
         return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
 
 

@@ -54,6 +54,33 @@ class ScriptReverb(nn.Module):
         return torch.ops.ddsp_hip.reverb_apply(x, spec, self.length)
 
 
+class ScriptGRUDecoder(nn.Module):
+    """GRUDecoder (decoder.py:9-68) for TorchScript: the recurrence through torch.ops.ddsp_hip.gru
+    (shares the source module's submodules and parameters)."""
+
+    def __init__(self, d):
+        super().__init__()
+        self.f0_mlp = d.f0_mlp
+        self.loudness_mlp = d.loudness_mlp
+        self.gru = d.gru
+        self.out_mlp = d.out_mlp
+        self.register_buffer("cache_gru", d.cache_gru)
+        self.native = bool(d.gru.hidden_size % 64 == 0)  # the step kernel's shapes (core.gru_supported)
+
+    def forward(self, f0: torch.Tensor, loudness: torch.Tensor, realtime: bool = False) -> torch.Tensor:
+        hidden = torch.cat([self.f0_mlp(f0), self.loudness_mlp(loudness)], -1)
+        g = self.gru
+        h0 = self.cache_gru if realtime else None
+        if self.native:
+            out, h_last = torch.ops.ddsp_hip.gru(hidden, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0,
+                                                 h0)
+        else:
+            out, h_last = g(hidden, h0)
+        if realtime:
+            self.cache_gru.copy_(h_last)
+        return self.out_mlp(torch.cat([out, f0, loudness], -1))
+
+
 class ScriptDecoder(nn.Module):
     """DDSPDecoder (decoder.py:70-136) restated for TorchScript; same parameter/buffer names."""
 
@@ -61,7 +88,7 @@ class ScriptDecoder(nn.Module):
         super().__init__()
         self.register_buffer("sample_rate", m.sample_rate.clone())
         self.register_buffer("block_size", m.block_size.clone())
-        self.decoder = m.decoder
+        self.decoder = ScriptGRUDecoder(m.decoder)
         self.harmonic_proj = m.harmonic_proj
         self.noise_proj = m.noise_proj
         self.reverb = ScriptReverb(m.reverb)

@@ -159,6 +159,14 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
+ * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,
+ * computed by the caller's GEMM), W_hh[3H,H], b_hh[3H] in torch's (r, z, n) order; h0 [B,H]
+ * (NULL = zeros); h_last [B,H] (nullable) receives h_T.  One launch per time step.  Forward
+ * only (inference and the realtime host); hidden % 64 == 0 (else DDSP_HIP_ERANGE). */
+int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
+                         float* h_last, int64_t batch, int64_t steps, int64_t hidden, void* stream);
+
 /* ---------------- training loss: ddsp/core.py:27-41 multiscale_fft ----------------
  * One scale of multiscale_fft: |torch.stft(x, n_fft, hop, n_fft, hann(n_fft), center=True
  * (reflect), normalized=True)| for x[batch, n_samples] (n_fft a power of two in [16, 4096],
