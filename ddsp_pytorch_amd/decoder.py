@@ -36,20 +36,32 @@ class GRUDecoder(nn.Module):
         self.out_mlp = mlp(hidden_size + 2, hidden_size, 3)
 
     def forward(self, f0, loudness, realtime: bool = False):
-        hidden = torch.cat([self.f0_mlp(f0), self.loudness_mlp(loudness)], -1)
-        # the recurrence on the gfx950 step kernel for inference; torch's GRU (MIOpen) when
-        # autograd needs its backward
-        native = hidden.is_cuda and core.gru_supported(self.gru) and not (
-            torch.is_grad_enabled() and (hidden.requires_grad or self.gru.weight_hh_l0.requires_grad))
-        if realtime:
-            if native:
-                gru_out, cache = core.gru(hidden, self.gru, self.cache_gru)
-            else:
-                gru_out, cache = self.gru(hidden, self.cache_gru)
-            self.cache_gru.copy_(cache)
-        else:
-            gru_out = core.gru(hidden, self.gru)[0] if native else self.gru(hidden)[0]
-        return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
+        return gru_decoder_forward(self, f0, loudness, None, realtime)
+
+
+def _gru(mod, hidden, h0):
+    """mod.gru(hidden[, h0]) with the recurrence on the gfx950 step kernel for inference; torch's
+    GRU (MIOpen) when autograd needs its backward or the shape is outside the kernel's."""
+    native = hidden.is_cuda and core.gru_supported(mod.gru) and not (
+        torch.is_grad_enabled() and (hidden.requires_grad or mod.gru.weight_hh_l0.requires_grad))
+    if native:
+        return core.gru(hidden, mod.gru, h0)
+    return mod.gru(hidden, h0) if h0 is not None else mod.gru(hidden)
+
+
+def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
+    """ddsp/models/decoder.py:43-68 GRUDecoder.forward (incl. the optional z projection), the GRU on
+    the step kernel for inference.  install() binds it to the reference's GRUDecoder too."""
+    hidden = torch.cat([self.f0_mlp(f0), self.loudness_mlp(loudness)], -1)
+    if getattr(self, "add_z", False):
+        assert z is not None
+        hidden = torch.cat([hidden, self.z_mlp(z)], -1)
+    if realtime:
+        gru_out, cache = _gru(self, hidden, self.cache_gru)
+        self.cache_gru.copy_(cache)
+    else:
+        gru_out = _gru(self, hidden, None)[0]
+    return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
 
 
 class DDSPDecoder(nn.Module):
