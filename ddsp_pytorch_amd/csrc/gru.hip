@@ -33,7 +33,8 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
                                                        int B, int H, int64_t xp_ld) {
   extern __shared__ float smem[];
   constexpr int R = 3 * kHS;
-  float* part = smem;                 // [kKC][R][kBS]
+  float* W = smem;                    // [R][H]
+  float* part = smem + R * H;         // [kKC][R][kBS]
   const int j0 = blockIdx.x * kHS, b0 = blockIdx.y * kBS;
   const int tid = threadIdx.x;
   const int bl = tid % kBS, c = tid / kBS;
@@ -44,23 +45,29 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  // W straight from global (L2/MALL): the lanes of a wave share two k-chunks, so each 16-B W load
-  // is two distinct addresses per wave; no LDS staging and no barrier before the dot products
-  const float* wrow[R];
+  for (int k0 = 0; k0 < KLr; k0 += 32) {
+    // issue up to 8 16-B h loads first (the first batch overlaps the W staging below)
+    float4 hv[8];
 #pragma unroll
-  for (int r = 0; r < R; ++r) wrow[r] = w_hh + (int64_t)((r / kHS) * H + j0 + (r % kHS)) * H + c * KLr;
-  for (int k0 = 0; k0 < KLr; k0 += 16) {
-    float4 hv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 8; ++q)
       hv[q] = (hv_ok && k0 + 4 * q < KLr) ? *reinterpret_cast<const float4*>(hrow + k0 + 4 * q)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k0 == 0) {
+      // rows: gate g of unit u is W_hh row g*H + j0 + u
+      for (int i = tid; i < R * H / 4; i += kNT) {
+        const int r = (4 * i) / H, k = 4 * i - r * H;
+        const int g = r / kHS, u = r - g * kHS;
+        *reinterpret_cast<float4*>(W + r * H + k) =
+            *reinterpret_cast<const float4*>(w_hh + (int64_t)(g * H + j0 + u) * H + k);
+      }
+      __syncthreads();
+    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 8; ++q) {
       if (k0 + 4 * q < KLr) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const float4 wv = *reinterpret_cast<const float4*>(wrow[r] + k0 + 4 * q);
+          const float4 wv = *reinterpret_cast<const float4*>(W + r * H + c * KLr + k0 + 4 * q);
           acc[r] = fmaf(wv.x, hv[q].x, fmaf(wv.y, hv[q].y, fmaf(wv.z, hv[q].z, fmaf(wv.w, hv[q].w, acc[r]))));
         }
       }
@@ -104,7 +111,7 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
   if (hidden % (4 * kKC) || hidden % kHS || hidden > 4096 || batch > 65535 * kBS) return DDSP_HIP_ERANGE;
   const int H = (int)hidden, B = (int)batch;
-  const size_t shm = sizeof(float) * ((size_t)kKC * 3 * kHS * kBS);
+  const size_t shm = sizeof(float) * ((size_t)3 * kHS * H + (size_t)kKC * 3 * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
   const int64_t row = steps * hidden;  // out[b] row stride: [B, T, H]
   for (int64_t t = 0; t < steps; ++t) {
