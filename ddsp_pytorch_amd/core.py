@@ -449,22 +449,24 @@ def gru_supported(gru_module):
 
 def gru(x, gru_module, h0=None):
     """torch.nn.GRU(x, h0) forward (1 layer, batch_first) -> (out [B,T,H], h_T [1,B,H]): the input
-    projection for all steps as one GEMM, the recurrence on the gfx950 step kernel.  Inference
-    only (callers keep torch's GRU where autograd needs its backward)."""
+    projection for all steps as one GEMM, the recurrence on the gfx950 step kernel; under autograd
+    the backward (BPTT) runs on the step kernels too (grad.GRUFn)."""
     _dev(x)
     if not gru_supported(gru_module):
         raise RuntimeError("gru: one layer, batch_first, unidirectional, with bias and hidden % 64 == 0 expected")
+    g = gru_module
+    params = (g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)
+    if _wants_grad(x, h0, *params):
+        return _grad.GRUFn.apply(x, *params, h0)
     B, T, _ = x.shape
-    H = gru_module.hidden_size
-    w_ih, w_hh = gru_module.weight_ih_l0, gru_module.weight_hh_l0
-    b_ih, b_hh = gru_module.bias_ih_l0, gru_module.bias_hh_l0
-    with torch.no_grad():
-        xp = torch.addmm(b_ih, x.reshape(B * T, -1), w_ih.t()).view(B, T, 3 * H)
-        out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
-        h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
-        h0c = _c(h0.reshape(B, H)) if h0 is not None else None
-        _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
-                  _lib.ptr(h_last), B, T, H, _lib.stream_of(out))
+    H = g.hidden_size
+    w_ih, w_hh, b_ih, b_hh = params
+    xp = torch.addmm(b_ih, x.reshape(B * T, -1), w_ih.t()).view(B, T, 3 * H)
+    out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
+    h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
+    h0c = _c(h0.reshape(B, H)) if h0 is not None else None
+    _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
+              _lib.ptr(h_last), None, B, T, H, _lib.stream_of(out))
     return out, h_last
 
 

@@ -30,7 +30,8 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__ xp, const float* __restrict__ w_hh,
                                                        const float* __restrict__ b_hh, const float* __restrict__ h_prev,
                                                        int64_t hp_ld, float* __restrict__ h_out, int64_t ho_ld,
-                                                       int B, int H, int64_t xp_ld) {
+                                                       int B, int H, int64_t xp_ld, float* __restrict__ save,
+                                                       int64_t save_plane) {
   extern __shared__ float smem[];
   constexpr int R = 3 * kHS;
   float* W = smem;                    // [R][H]
@@ -93,6 +94,126 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
       const float n = tanhf(xr[2 * H + j] + r * (hn + b_hh[2 * H + j]));
       const float hp = h_prev ? h_prev[(int64_t)bi * hp_ld + j] : 0.0f;
       h_out[(int64_t)bi * ho_ld + j] = (1.0f - z) * n + z * hp;
+      if (save) {  // training: r, z, n and W_hn h + b_hn of this step, [4][B, T, H] (same row layout as h_out)
+        float* sv = save + (int64_t)bi * ho_ld + j;
+        sv[0] = r;
+        sv[save_plane] = z;
+        sv[2 * save_plane] = n;
+        sv[3 * save_plane] = hn + b_hh[2 * H + j];
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Backward (BPTT) of the recurrence, for training.  With dh the total gradient reaching h_t:
+//   dn = dh (1 - z), dz = dh (h_{t-1} - n), da_n = dn (1 - n^2), da_z = dz z (1 - z),
+//   da_r = da_n hn r (1 - r), dhn = da_n r     (hn = W_hn h_{t-1} + b_hn)
+//   dxp_t = (da_r, da_z, da_n)   -> the input projection's gradient (GEMMs on the host side)
+//   dG_t  = (da_r, da_z, dhn)    -> dW_hh = sum_t dG_t^T h_{t-1}, db_hh = sum_t dG_t (host GEMMs)
+//   dh_{t-1} = dh z + W_hh^T dG_t + dout_{t-1}
+// One launch per step: the transposed product for a slice of units x a batch tile, then, for the
+// same (b, unit) elements, the step t-1 elementwise part (its dxp and dG_n) so the next launch
+// finds dG_{t-1} ready.
+
+// the elementwise part at step t for element (b, j), given the total dh: writes dxp, dGn
+__device__ __forceinline__ void gru_bwd_elem(const float* __restrict__ save, int64_t plane, int64_t idx, float hprev,
+                                             float dh, float* __restrict__ dxp, int64_t xi, int H,
+                                             float* __restrict__ dgn) {
+  const float r = save[idx], z = save[plane + idx], n = save[2 * plane + idx], hn = save[3 * plane + idx];
+  const float dn = dh * (1.0f - z);
+  const float dz = dh * (hprev - n);
+  const float dan = dn * (1.0f - n * n);
+  const float daz = dz * z * (1.0f - z);
+  const float dar = dan * hn * r * (1.0f - r);
+  dxp[xi] = dar;
+  dxp[xi + H] = daz;
+  dxp[xi + 2 * H] = dan;
+  dgn[idx] = dan * r;
+}
+
+// step T-1's elementwise part from dh = dout[:, T-1] (+ dh_last); grid-stride over B*H
+__global__ void gru_bwd_init_kernel(const float* __restrict__ dout, const float* __restrict__ dh_last,
+                                    const float* __restrict__ out, const float* __restrict__ h0,
+                                    const float* __restrict__ save, int64_t plane, float* __restrict__ dxp,
+                                    float* __restrict__ dgn, float* __restrict__ dh_buf, int B, int T, int H) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)B * H;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / H, j = e - b * H;
+    const int64_t idx = (b * T + (T - 1)) * H + j;
+    float dh = dout ? dout[idx] : 0.0f;
+    if (dh_last) dh += dh_last[e];
+    const float hprev = T >= 2 ? out[idx - H] : (h0 ? h0[e] : 0.0f);
+    dh_buf[e] = dh;
+    gru_bwd_elem(save, plane, idx, hprev, dh, dxp, (b * T + (T - 1)) * 3 * H + j, H, dgn);
+  }
+}
+
+// step t (>= 1): dh_{t-1} for units [i0, i0+kHS) x a batch tile, then step t-1's elementwise
+// part; t == 0 writes dh0 only.  grid (H / kHS, ceil(B / kBS)); LDS: W_hh columns [3H][kHS] +
+// partials [kKC][kHS][kBS]
+__global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
+    const float* __restrict__ w_hh, const float* __restrict__ save, int64_t plane, const float* __restrict__ dout,
+    const float* __restrict__ out, const float* __restrict__ h0, float* __restrict__ dxp, float* __restrict__ dgn,
+    const float* __restrict__ dh_in, float* __restrict__ dh_outbuf, float* __restrict__ dh0, int B, int T, int H,
+    int t) {
+  extern __shared__ float smem[];
+  const int K = 3 * H;
+  float* Wt = smem;                 // [K][kHS]: Wt[k][u] = W_hh[k][i0 + u]
+  float* part = smem + K * kHS;     // [kKC][kHS][kBS]
+  const int i0 = blockIdx.x * kHS, b0 = blockIdx.y * kBS;
+  const int tid = threadIdx.x;
+  const int bl = tid % kBS, c = tid / kBS;
+  const int b = b0 + bl;
+  const int KLr = K / kKC;  // this thread's reduction range (K % (4 kKC) == 0)
+  // dG_t row of this batch element: (dxp_r, dxp_z) = dG_r, dG_z; dG_n = dgn
+  float acc[kHS];
+#pragma unroll
+  for (int u = 0; u < kHS; ++u) acc[u] = 0.0f;
+  for (int k = tid; k < K; k += kNT)
+    *reinterpret_cast<float4*>(Wt + k * kHS) = *reinterpret_cast<const float4*>(w_hh + (int64_t)k * H + i0);
+  __syncthreads();
+  if (b < B) {
+    const float* gx = dxp + ((int64_t)b * T + t) * 3 * H;  // [3H]: r, z rows are dG
+    const float* gn = dgn + ((int64_t)b * T + t) * H;      // [H]: dG_n
+    const int k0 = c * KLr;
+    for (int k = k0; k < k0 + KLr; k += 4) {
+      const float4 g4 = k < 2 * H ? *reinterpret_cast<const float4*>(gx + k)
+                                  : *reinterpret_cast<const float4*>(gn + (k - 2 * H));
+      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = *reinterpret_cast<const float4*>(Wt + (k + q) * kHS);
+        acc[0] = fmaf(w.x, gv[q], acc[0]);
+        acc[1] = fmaf(w.y, gv[q], acc[1]);
+        acc[2] = fmaf(w.z, gv[q], acc[2]);
+        acc[3] = fmaf(w.w, gv[q], acc[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kHS; ++u) part[(c * kHS + u) * kBS + bl] = acc[u];
+  __syncthreads();
+  if (tid < kHS * kBS) {
+    const int u = tid / kBS, bb = tid - u * kBS;
+    const int bi = b0 + bb, i = i0 + u;
+    if (bi < B) {
+      float s = 0.0f;
+      for (int cc = 0; cc < kKC; ++cc) s += part[(cc * kHS + u) * kBS + bb];
+      const int64_t e = (int64_t)bi * H + i;
+      const int64_t idx_t = ((int64_t)bi * T + t) * H + i;
+      // dh_{t-1} = dh_t z_t + W_hh^T dG_t + dout_{t-1}
+      float dh = dh_in[e] * save[plane + idx_t] + s;
+      if (t == 0) {
+        if (dh0) dh0[e] = dh;
+      } else {
+        const int64_t idx = idx_t - H;  // step t-1
+        if (dout) dh += dout[idx];
+        dh_outbuf[e] = dh;
+        const float hprev = t >= 2 ? out[idx - H] : (h0 ? h0[e] : 0.0f);
+        gru_bwd_elem(save, plane, idx, hprev, dh, dxp, ((int64_t)bi * T + (t - 1)) * 3 * H + i, H, dgn);
+      }
     }
   }
 }
@@ -105,7 +226,7 @@ using namespace ddsp;
 extern "C" {
 
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
-                         float* h_last, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
+                         float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
   if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
@@ -118,7 +239,8 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
     const float* hp = t == 0 ? h0 : out + (t - 1) * hidden;
     const int64_t hp_ld = t == 0 ? hidden : row;
     hipLaunchKernelGGL(gru_step_kernel, grid, dim3(kNT), shm, reinterpret_cast<hipStream_t>(stream),
-                       xp + t * 3 * hidden, w_hh, b_hh, hp, hp_ld, out + t * hidden, row, B, H, steps * 3 * hidden);
+                       xp + t * 3 * hidden, w_hh, b_hh, hp, hp_ld, out + t * hidden, row, B, H, steps * 3 * hidden,
+                       gates ? gates + t * hidden : nullptr, batch * steps * hidden);
     int st = launch_status();
     if (st) return st;
   }
@@ -127,6 +249,34 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
                                     sizeof(float) * hidden, batch, hipMemcpyDeviceToDevice,
                                     reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) return DDSP_HIP_ELAUNCH;
+  }
+  return DDSP_HIP_OK;
+}
+
+int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
+                          const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
+                          float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || steps == 0) return DDSP_HIP_OK;
+  if (!w_hh || !gates || !out || !grad_xp || !grad_gn) return DDSP_HIP_EINVAL;
+  if (hidden % (4 * kKC) || hidden % kHS || hidden > 4096 || batch > 65535 * kBS) return DDSP_HIP_ERANGE;
+  if (!workspace || workspace_bytes < 2 * sizeof(float) * (size_t)batch * hidden) return DDSP_HIP_EWORKSPACE;
+  const int H = (int)hidden, B = (int)batch, T = (int)steps;
+  const int64_t plane = batch * steps * hidden;
+  float* dhb[2] = {reinterpret_cast<float*>(workspace), reinterpret_cast<float*>(workspace) + batch * hidden};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g1 = (unsigned)std::min<int64_t>((batch * hidden + 255) / 256, 65535);
+  hipLaunchKernelGGL(gru_bwd_init_kernel, dim3(g1), dim3(256), 0, st, grad_out, grad_h_last, out, h0, gates, plane,
+                     grad_xp, grad_gn, dhb[(T - 1) & 1], B, T, H);
+  int r = launch_status();
+  if (r) return r;
+  const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)kKC * kHS * kBS);
+  const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
+  for (int t = T - 1; t >= 0; --t) {
+    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(kNT), shm, st, w_hh, gates, plane, grad_out, out, h0, grad_xp,
+                       grad_gn, dhb[t & 1], dhb[(t - 1) & 1], grad_h0, B, T, H, t);
+    if ((r = launch_status())) return r;
   }
   return DDSP_HIP_OK;
 }

@@ -287,7 +287,7 @@ std::tuple<at::Tensor, at::Tensor> gru(const at::Tensor& x, const at::Tensor& w_
   at::Tensor whh = c16(w_hh), bhh = c16(b_hh);
   ok(ddsp_hip_gru_forward(xp.data_ptr<float>(), whh.data_ptr<float>(), bhh.data_ptr<float>(),
                           h0c.defined() ? h0c.data_ptr<float>() : nullptr, out.data_ptr<float>(),
-                          h_last.data_ptr<float>(), B, T, H, stream_of(x)),
+                          h_last.data_ptr<float>(), nullptr, B, T, H, stream_of(x)),
      "gru_forward");
   return {out, h_last};
 }

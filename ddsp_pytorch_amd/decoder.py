@@ -40,11 +40,9 @@ class GRUDecoder(nn.Module):
 
 
 def _gru(mod, hidden, h0):
-    """mod.gru(hidden[, h0]) with the recurrence on the gfx950 step kernel for inference; torch's
-    GRU (MIOpen) when autograd needs its backward or the shape is outside the kernel's."""
-    native = hidden.is_cuda and core.gru_supported(mod.gru) and not (
-        torch.is_grad_enabled() and (hidden.requires_grad or mod.gru.weight_hh_l0.requires_grad))
-    if native:
+    """mod.gru(hidden[, h0]) with the recurrence (and, under autograd, its BPTT) on the gfx950 step
+    kernels; torch's GRU only for shapes outside the kernel's (hidden % 64 != 0)."""
+    if hidden.is_cuda and core.gru_supported(mod.gru):
         return core.gru(hidden, mod.gru, h0)
     return mod.gru(hidden, h0) if h0 is not None else mod.gru(hidden)
 

@@ -403,3 +403,52 @@ class StftMagFn(_F):
         _lib.call("stft_magnitude_backward", _lib.ptr(core._c(x.detach())), _lib.ptr(gM), _lib.ptr(dx), B, T,
                   ctx.n_fft, ctx.hop, _lib.ptr(ws), ws.numel(), _lib.stream_of(dx))
         return dx, None, None
+
+
+# ------------------------------------------------------------------------------------------
+class GRUFn(_F):
+    """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 step kernels
+    (csrc/gru.hip); the input projection and the weight gradients are plain GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0):
+        B, T, I = x.shape
+        H = w_hh.shape[1]
+        xp = torch.addmm(b_ih, x.reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
+        out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
+        h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
+        gates = torch.empty(4, B, T, H, dtype=torch.float32, device=x.device)
+        h0c = core._c(h0.reshape(B, H)) if h0 is not None else None
+        _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(core._c(w_hh)), _lib.ptr(core._c(b_hh)), _lib.ptr(h0c),
+                  _lib.ptr(out), _lib.ptr(h_last), _lib.ptr(gates), B, T, H, _lib.stream_of(out))
+        ctx.save_for_backward(x, w_ih, w_hh, out, gates, h0c if h0c is not None else torch.empty(0))
+        ctx.has_h0 = h0 is not None
+        ctx.h0_shape = h0.shape if h0 is not None else None
+        return out, h_last
+
+    @staticmethod
+    def backward(ctx, g_out, g_hlast):
+        x, w_ih, w_hh, out, gates, h0c = ctx.saved_tensors
+        B, T, I = x.shape
+        H = w_hh.shape[1]
+        h0p = h0c if ctx.has_h0 else None
+        dxp = torch.empty(B, T, 3 * H, dtype=torch.float32, device=x.device)
+        dgn = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
+        dh0 = torch.empty(B, H, dtype=torch.float32, device=x.device) if ctx.has_h0 else None
+        ws = core._workspace(2 * 4 * B * H, x.device)
+        go = core._c(g_out) if g_out is not None else None
+        gh = core._c(g_hlast.reshape(B, H)) if g_hlast is not None else None
+        _lib.call("gru_backward", _lib.ptr(core._c(w_hh)), _lib.ptr(gates), _lib.ptr(out), _lib.ptr(h0p), _lib.ptr(go),
+                  _lib.ptr(gh), _lib.ptr(dxp), _lib.ptr(dgn), _lib.ptr(dh0), B, T, H, _lib.ptr(ws), ws.numel(),
+                  _lib.stream_of(dxp))
+        dxp2 = dxp.view(B * T, 3 * H)
+        dG = torch.cat([dxp[..., :2 * H], dgn], -1).view(B * T, 3 * H)
+        hprev = torch.cat([(h0p.view(B, 1, H) if h0p is not None else torch.zeros(B, 1, H, device=x.device)),
+                           out[:, :-1]], 1).reshape(B * T, H)
+        dx = (dxp2 @ w_ih).view(B, T, I) if ctx.needs_input_grad[0] else None
+        dw_ih = dxp2.t() @ x.reshape(B * T, I) if ctx.needs_input_grad[1] else None
+        dw_hh = dG.t() @ hprev if ctx.needs_input_grad[2] else None
+        db_ih = dxp2.sum(0) if ctx.needs_input_grad[3] else None
+        db_hh = dG.sum(0) if ctx.needs_input_grad[4] else None
+        dh0r = dh0.view(ctx.h0_shape) if (ctx.has_h0 and ctx.needs_input_grad[5]) else None
+        return dx, dw_ih, dw_hh, db_ih, db_hh, dh0r

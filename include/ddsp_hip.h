@@ -162,10 +162,19 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
 /* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
  * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,
  * computed by the caller's GEMM), W_hh[3H,H], b_hh[3H] in torch's (r, z, n) order; h0 [B,H]
- * (NULL = zeros); h_last [B,H] (nullable) receives h_T.  One launch per time step.  Forward
- * only (inference and the realtime host); hidden % 64 == 0 (else DDSP_HIP_ERANGE). */
+ * (NULL = zeros); h_last [B,H] (nullable) receives h_T; gates (nullable, training) [4][B,T,H]
+ * receives r, z, n and W_hn h + b_hn of every step for the backward.  One launch per time
+ * step; hidden % 64 == 0 (else DDSP_HIP_ERANGE).
+ * Backward (BPTT): from grad_out[B,T,H] (nullable) and grad_h_last[B,H] (nullable) ->
+ * grad_xp[B,T,3H] (gradient of the input projection: dW_ih, db_ih, dx are GEMMs of it),
+ * grad_gn[B,T,H] (with grad_xp's r and z planes, the gradient of W_hh h + b_hh: dW_hh and db_hh
+ * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace 2*B*H floats. */
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
-                         float* h_last, int64_t batch, int64_t steps, int64_t hidden, void* stream);
+                         float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream);
+int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
+                          const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
+                          float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* ---------------- training loss: ddsp/core.py:27-41 multiscale_fft ----------------
  * One scale of multiscale_fft: |torch.stft(x, n_fft, hop, n_fft, hann(n_fft), center=True

@@ -51,13 +51,43 @@ def test_gru_torch_op(dd):
     assert relerr(out, ref) < 1e-5 and relerr(h, rh) < 1e-5
 
 
-def test_decoder_uses_native_gru_for_inference_only(dd):
-    """DDSPDecoder: the step kernel under no_grad, torch's GRU (with its backward) when training."""
+def test_decoder_gru_inference_and_training_paths_agree(dd):
+    """DDSPDecoder: the step kernel under no_grad and, with autograd, the BPTT-capable Function."""
     m = dd.DDSPDecoder(64, 16, 65, 48000, 64, False).cuda()
     f0 = torch.full((2, 8, 1), 220.0, device="cuda")
     lo = torch.randn(2, 8, 1, device="cuda")
     with torch.no_grad():
         a = m.decoder(f0, lo)
-    b = m.decoder(f0, lo)  # grad enabled: nn.GRU path
+    b = m.decoder(f0, lo)  # grad enabled: the BPTT-capable path
     assert b.requires_grad
     assert relerr(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,I,H,with_h0", [(64, 50, 1024, 512, False), (3, 17, 32, 64, True),
+                                             (40, 9, 96, 128, True)])
+def test_gru_backward(dd, B, T, I, H, with_h0):
+    """BPTT on the step kernels vs torch's GRU autograd on the CPU: every gradient."""
+    torch.manual_seed(B + T + H)
+    g = torch.nn.GRU(I, H, batch_first=True)
+    x = torch.randn(B, T, I)
+    h0 = torch.randn(1, B, H) * 0.5 if with_h0 else None
+    w = torch.randn(B, T, H)
+    wl = torch.randn(1, B, H)
+    xc = x.clone().requires_grad_(True)
+    h0c = h0.clone().requires_grad_(True) if with_h0 else None
+    out, hl = g(xc, h0c) if with_h0 else g(xc)
+    ((out * w).sum() + (hl * wl).sum()).backward()
+    ref = {n: p.grad.clone() for n, p in g.named_parameters()}
+    gg = g.cuda()
+    for p in gg.parameters():
+        p.grad = None
+    xg = x.cuda().requires_grad_(True)
+    h0g = h0.cuda().requires_grad_(True) if with_h0 else None
+    og, hg = dd.core.gru(xg, gg, h0g)
+    ((og * w.cuda()).sum() + (hg * wl.cuda()).sum()).backward()
+    assert relerr(og, out) < 1e-5
+    assert relerr(xg.grad, xc.grad) < 1e-5, relerr(xg.grad, xc.grad)
+    for n, p in gg.named_parameters():
+        assert relerr(p.grad, ref[n]) < 1e-5, (n, relerr(p.grad, ref[n]))
+    if with_h0:
+        assert relerr(h0g.grad, h0c.grad) < 1e-5, relerr(h0g.grad, h0c.grad)
