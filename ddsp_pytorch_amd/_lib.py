@@ -47,6 +47,7 @@ SIGNATURES = {
     "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P]),
     "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_gru_forward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
+    "ddsp_hip_gru_backward_workspace_size": (_SZ, [_I64, _I64]),
     "ddsp_hip_gru_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
     # multiscale STFT (training loss)
     "ddsp_hip_stft_frames": (_I64, [_I64, _I64]),

@@ -133,6 +133,19 @@ __device__ __forceinline__ void gru_bwd_elem(const float* __restrict__ save, int
   dgn[idx] = dan * r;
 }
 
+// WT[i][k] = W_hh[k][i] (H x 3H), so the backward's per-unit columns are contiguous rows; 32x32 tiles
+__global__ void __launch_bounds__(256) transpose_kernel(const float* __restrict__ w, float* __restrict__ wt, int rows,
+                                                        int cols) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8)
+    if (r0 + y < rows && c0 + tx < cols) tile[y][tx] = w[(int64_t)(r0 + y) * cols + c0 + tx];
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8)
+    if (c0 + y < cols && r0 + tx < rows) wt[(int64_t)(c0 + y) * rows + r0 + tx] = tile[tx][y];
+}
+
 // step T-1's elementwise part from dh = dout[:, T-1] (+ dh_last); grid-stride over B*H
 __global__ void gru_bwd_init_kernel(const float* __restrict__ dout, const float* __restrict__ dh_last,
                                     const float* __restrict__ out, const float* __restrict__ h0,
@@ -154,7 +167,7 @@ __global__ void gru_bwd_init_kernel(const float* __restrict__ dout, const float*
 // part; t == 0 writes dh0 only.  grid (H / kHS, ceil(B / kBS)); LDS: W_hh columns [3H][kHS] +
 // partials [kKC][kHS][kBS]
 __global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
-    const float* __restrict__ w_hh, const float* __restrict__ save, int64_t plane, const float* __restrict__ dout,
+    const float* __restrict__ w_t, const float* __restrict__ save, int64_t plane, const float* __restrict__ dout,
     const float* __restrict__ out, const float* __restrict__ h0, float* __restrict__ dxp, float* __restrict__ dgn,
     const float* __restrict__ dh_in, float* __restrict__ dh_outbuf, float* __restrict__ dh0, int B, int T, int H,
     int t) {
@@ -171,24 +184,43 @@ __global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
   float acc[kHS];
 #pragma unroll
   for (int u = 0; u < kHS; ++u) acc[u] = 0.0f;
-  for (int k = tid; k < K; k += kNT)
-    *reinterpret_cast<float4*>(Wt + k * kHS) = *reinterpret_cast<const float4*>(w_hh + (int64_t)k * H + i0);
+  // rows i0..i0+kHS of W_hh^T (contiguous), stored interleaved [k][u] for float4 reads
+  for (int e = tid; e < kHS * K / 4; e += kNT) {
+    const int u = e / (K / 4), k = 4 * (e - u * (K / 4));
+    const float4 v = *reinterpret_cast<const float4*>(w_t + (int64_t)(i0 + u) * K + k);
+    Wt[(k + 0) * kHS + u] = v.x;
+    Wt[(k + 1) * kHS + u] = v.y;
+    Wt[(k + 2) * kHS + u] = v.z;
+    Wt[(k + 3) * kHS + u] = v.w;
+  }
   __syncthreads();
   if (b < B) {
     const float* gx = dxp + ((int64_t)b * T + t) * 3 * H;  // [3H]: r, z rows are dG
     const float* gn = dgn + ((int64_t)b * T + t) * H;      // [H]: dG_n
     const int k0 = c * KLr;
-    for (int k = k0; k < k0 + KLr; k += 4) {
-      const float4 g4 = k < 2 * H ? *reinterpret_cast<const float4*>(gx + k)
-                                  : *reinterpret_cast<const float4*>(gn + (k - 2 * H));
-      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+    for (int kb = k0; kb < k0 + KLr; kb += 32) {
+      float4 g4[8];  // issue 8 16-B loads before consuming them
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 w = *reinterpret_cast<const float4*>(Wt + (k + q) * kHS);
-        acc[0] = fmaf(w.x, gv[q], acc[0]);
-        acc[1] = fmaf(w.y, gv[q], acc[1]);
-        acc[2] = fmaf(w.z, gv[q], acc[2]);
-        acc[3] = fmaf(w.w, gv[q], acc[3]);
+      for (int q = 0; q < 8; ++q) {
+        const int k = kb + 4 * q;
+        g4[q] = k >= k0 + KLr ? make_float4(0.f, 0.f, 0.f, 0.f)
+                              : (k < 2 * H ? *reinterpret_cast<const float4*>(gx + k)
+                                           : *reinterpret_cast<const float4*>(gn + (k - 2 * H)));
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = kb + 4 * q;
+        if (k < k0 + KLr) {
+          const float gv[4] = {g4[q].x, g4[q].y, g4[q].z, g4[q].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float4 w = *reinterpret_cast<const float4*>(Wt + (k + e) * kHS);
+            acc[0] = fmaf(w.x, gv[e], acc[0]);
+            acc[1] = fmaf(w.y, gv[e], acc[1]);
+            acc[2] = fmaf(w.z, gv[e], acc[2]);
+            acc[3] = fmaf(w.w, gv[e], acc[3]);
+          }
+        }
       }
     }
   }
@@ -253,6 +285,11 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   return DDSP_HIP_OK;
 }
 
+size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden) {
+  if (batch < 1 || hidden < 1) return 0;
+  return sizeof(float) * ((size_t)2 * batch * hidden + (size_t)3 * hidden * hidden);
+}
+
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
                           float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, void* workspace,
@@ -261,11 +298,14 @@ int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* ou
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!w_hh || !gates || !out || !grad_xp || !grad_gn) return DDSP_HIP_EINVAL;
   if (hidden % (4 * kKC) || hidden % kHS || hidden > 4096 || batch > 65535 * kBS) return DDSP_HIP_ERANGE;
-  if (!workspace || workspace_bytes < 2 * sizeof(float) * (size_t)batch * hidden) return DDSP_HIP_EWORKSPACE;
+  if (!workspace || workspace_bytes < ddsp_hip_gru_backward_workspace_size(batch, hidden)) return DDSP_HIP_EWORKSPACE;
   const int H = (int)hidden, B = (int)batch, T = (int)steps;
   const int64_t plane = batch * steps * hidden;
   float* dhb[2] = {reinterpret_cast<float*>(workspace), reinterpret_cast<float*>(workspace) + batch * hidden};
+  float* w_t = reinterpret_cast<float*>(workspace) + 2 * batch * hidden;  // [H][3H]
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((H + 31) / 32), (unsigned)((3 * H + 31) / 32)), dim3(256), 0,
+                     st, w_hh, w_t, 3 * H, H);
   const unsigned g1 = (unsigned)std::min<int64_t>((batch * hidden + 255) / 256, 65535);
   hipLaunchKernelGGL(gru_bwd_init_kernel, dim3(g1), dim3(256), 0, st, grad_out, grad_h_last, out, h0, gates, plane,
                      grad_xp, grad_gn, dhb[(T - 1) & 1], B, T, H);
@@ -274,7 +314,7 @@ int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* ou
   const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)kKC * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
   for (int t = T - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(kNT), shm, st, w_hh, gates, plane, grad_out, out, h0, grad_xp,
+    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(kNT), shm, st, w_t, gates, plane, grad_out, out, h0, grad_xp,
                        grad_gn, dhb[t & 1], dhb[(t - 1) & 1], grad_h0, B, T, H, t);
     if ((r = launch_status())) return r;
   }

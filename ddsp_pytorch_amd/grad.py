@@ -435,7 +435,7 @@ class GRUFn(_F):
         dxp = torch.empty(B, T, 3 * H, dtype=torch.float32, device=x.device)
         dgn = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
         dh0 = torch.empty(B, H, dtype=torch.float32, device=x.device) if ctx.has_h0 else None
-        ws = core._workspace(2 * 4 * B * H, x.device)
+        ws = core._workspace(_lib.query("gru_backward_workspace_size", B, H), x.device)
         go = core._c(g_out) if g_out is not None else None
         gh = core._c(g_hlast.reshape(B, H)) if g_hlast is not None else None
         _lib.call("gru_backward", _lib.ptr(core._c(w_hh)), _lib.ptr(gates), _lib.ptr(out), _lib.ptr(h0p), _lib.ptr(go),

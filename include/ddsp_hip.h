@@ -168,9 +168,10 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
  * Backward (BPTT): from grad_out[B,T,H] (nullable) and grad_h_last[B,H] (nullable) ->
  * grad_xp[B,T,3H] (gradient of the input projection: dW_ih, db_ih, dx are GEMMs of it),
  * grad_gn[B,T,H] (with grad_xp's r and z planes, the gradient of W_hh h + b_hh: dW_hh and db_hh
- * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace 2*B*H floats. */
+ * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace: *_workspace_size. */
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                          float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream);
+size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden);
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
                           float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, void* workspace,
