@@ -64,6 +64,8 @@ def parse():
                    help="skip the training-step leg (synthesis forward + backward kernels)")
     p.add_argument("--no-loss-leg", action="store_true",
                    help="skip the multiscale spectral loss leg (forward + backward, both signals)")
+    p.add_argument("--no-model-train-leg", action="store_true",
+                   help="skip the full training step of train.py (DDSPDecoder + spectral loss + backward + Adam)")
     p.add_argument("--no-decoder-leg", action="store_true",
                    help="skip the full DDSPDecoder.forward leg (GRU/MLP + synthesis)")
     p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
@@ -249,6 +251,44 @@ def loss_leg(args, dev, reps=10):
                         "train.py's loss in torch; torch_stft: the reference's torch.stft (rocFFT) on the GPU"}
 
 
+def model_train_leg(args, inp, dev, reps=5):
+    """train.py:84-130's step at config 2's shape: DDSPDecoder.forward (hidden 512) -> fused spectral
+    loss -> backward -> Adam step, all gradients on the gfx950 kernels (synthesis VJPs, GRU BPTT,
+    STFT loss).  The network's MLPs/GEMMs are hipBLASLt through torch.  Random-init weights and a
+    synthetic target signal."""
+    from ddsp_pytorch_amd.decoder import DDSPDecoder
+    from ddsp_pytorch_amd.loss import spectral_loss
+    B, F, bs = args.batch, args.frames, args.block_size
+    torch.manual_seed(0)
+    model = DDSPDecoder(512, args.harmonics, args.bands, args.sample_rate, bs, True).to(dev).train()
+    model.noise_synth.noise_mode = "device"
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    sig = torch.randn(B, F * bs, device=dev) * 0.1
+    batch = {"pitch": inp["f0"], "loudness": torch.randn(B, F, 1, device=dev)}
+
+    def step():
+        out = model(batch)
+        loss = spectral_loss(sig, out["signal"].squeeze(-1))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loss = step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    assert torch.isfinite(loss)
+    del model, opt
+    return {"value": round(B * F * bs / t, 1), "unit": "samples/s", "ms_per_step": round(t * 1e3, 3),
+            "workload": f"train.py step: DDSPDecoder(hidden 512, H {args.harmonics}) fwd + spectral loss "
+                        f"(6 scales) + backward + Adam, batch {B} x {F} frames"}
+
+
 def decoder_leg(args, inp, dev, reps=10):
     """the full DDSPDecoder.forward rate, reported beside the synthesis path —
     GRU/MLP control network (hidden 512, torch on MIOpen/hipBLASLt) + the gfx950 synthesis."""
@@ -423,6 +463,9 @@ def main():
 
     if rank == 0 and not args.no_decoder_leg:
         result["decoder_forward"] = decoder_leg(args, inp, dev)
+
+    if rank == 0 and not args.no_model_train_leg:
+        result["model_train_step"] = model_train_leg(args, inp, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
