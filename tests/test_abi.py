@@ -74,3 +74,39 @@ def test_module_state_dict_keys_match_reference_layout():
               "decoder.f0_mlp.0.weight", "decoder.out_mlp.7.bias", "harmonic_proj.weight",
               "noise_proj.bias", "reverb.noise", "reverb.decay", "reverb.wet", "reverb.t"):
         assert k in keys, k
+
+
+def test_training_entry_points_reject_bad_arguments_without_launching():
+    """The backward / loss / GRU entry points validate before any HIP call (status codes only)."""
+    import ctypes
+    from ddsp_pytorch_amd import _lib
+    lib = _lib.load()
+    null = ctypes.c_void_p(0)
+    EINVAL, EWS, ERANGE = 1, 4, 5
+    # scale / upsample backward
+    assert lib.ddsp_hip_scale_function_backward(null, null, null, -1, 0.0, null) == EINVAL
+    assert lib.ddsp_hip_scale_function_backward(null, null, null, 0, 0.0, null) == 0
+    assert lib.ddsp_hip_upsample_backward(null, null, 1, 1, 1, 0, null) == EINVAL
+    # harmonic / noise / fused backward
+    assert lib.ddsp_hip_harmonic_synth_params_backward(null, null, null, null, 1, 2, 4, 64, 48000.0, null) == EINVAL
+    assert lib.ddsp_hip_harmonic_synth_params_backward(null, null, null, null, 0, 2, 4, 64, 48000.0, null) == 0
+    assert lib.ddsp_hip_filtered_noise_backward(null, null, 0, 0, 0, 0.0, null, null, 1, 1, 1, 512, null) == EINVAL
+    assert lib.ddsp_hip_synth_frames_backward(null, null, null, 0.0, null, 0, 0, null, null, null, null,
+                                              1, 2, 4, 65, 512, 48000.0, null) == EINVAL
+    # reverb backward: nothing requested / workspace
+    assert lib.ddsp_hip_reverb_backward(null, null, null, null, null, null, 1, 100, 10, null, 0, null) == EINVAL
+    # STFT: sizes outside the kernel's range, padding longer than the signal
+    assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 100, 25, null) == ERANGE
+    assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 8192, 2048, null) == ERANGE
+    assert lib.ddsp_hip_stft_magnitude(null, null, 1, 100, 256, 64, null) == EINVAL
+    assert lib.ddsp_hip_stft_frames(102400, 1024) == 101
+    n = (ctypes.c_int64 * 1)(512)
+    h = (ctypes.c_int64 * 1)(128)
+    assert lib.ddsp_hip_spectral_loss(null, null, 1, 1000, n, h, 1, null, null, null, 0, null) == EINVAL
+    assert lib.ddsp_hip_spectral_loss_workspace_size(2, 1000, n, h, 1) > 0
+    # GRU: hidden not a multiple of 64 is outside the step kernel's range
+    assert lib.ddsp_hip_gru_forward(null, null, null, null, null, null, null, 1, 4, 0, null) == EINVAL
+    assert lib.ddsp_hip_gru_forward(null, null, null, null, null, null, null, 0, 4, 64, null) == 0
+    one = ctypes.c_void_p(16)  # non-null placeholders: the range check comes first
+    assert lib.ddsp_hip_gru_forward(one, one, one, null, one, null, null, 1, 4, 96, null) == ERANGE
+    assert lib.ddsp_hip_gru_backward(one, one, one, null, null, null, one, one, null, 1, 4, 64, null, 0, null) == EWS
