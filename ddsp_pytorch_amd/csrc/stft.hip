@@ -217,6 +217,17 @@ __global__ void __launch_bounds__(256) spectral_loss_kernel(const float* __restr
   const float eps = 1e-7f;
   double lin = 0.0, lg = 0.0;
   float2 G[2][KPT];  // dL/dY_recon per bin, frames fa and fb
+  // both frames' samples are loaded up front: the second frame's global loads overlap the first FFT
+  float2 raw[2][16];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int f = fa + h;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t i = (int64_t)f * hop + t + Q * r - N / 2;
+      raw[h][r] = f < frames ? make_float2(reflect_load(rt, T, i), reflect_load(rr, T, i)) : make_float2(0.f, 0.f);
+    }
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int f = fa + h;
@@ -224,10 +235,8 @@ __global__ void __launch_bounds__(256) spectral_loss_kernel(const float* __restr
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = t + Q * r;
-      const float w = 0.5f - 0.5f * kTwiddle4096[2 * ((m * STEP) & 4095)];
-      const int64_t i = (int64_t)f * hop + m - N / 2;
-      v[r] = valid ? make_float2(reflect_load(rt, T, i) * w, reflect_load(rr, T, i) * w) : make_float2(0.f, 0.f);
+      const float w = 0.5f - 0.5f * kTwiddle4096[2 * (((t + Q * r) * STEP) & 4095)];
+      v[r] = make_float2(raw[h][r].x * w, raw[h][r].y * w);
     }
     fft_n<N, false>(v, lds, t);
     __syncthreads();
