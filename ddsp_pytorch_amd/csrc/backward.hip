@@ -243,10 +243,35 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
         int j = j0;
         for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
           const float2 p = wg[j], p1 = wg[j + 1];
+          // the 8 chains written stage by stage so the scheduler keeps them interleaved (ILP 8)
+          float x[2 * kKPT], t8[2 * kKPT], r8[2 * kKPT], q8[2 * kKPT];
 #pragma unroll
           for (int c = 0; c < kKPT; ++c) {
-            acc[c] = gsin_acc(p.x * kf[c], p.y, acc[c]);
-            acc2[c] = gsin_acc(p1.x * kf[c], p1.y, acc2[c]);
+            x[c] = p.x * kf[c];
+            x[kKPT + c] = p1.x * kf[c];
+          }
+#pragma unroll
+          for (int i = 0; i < 2 * kKPT; ++i) t8[i] = fmaf(x[i], kInvPi, kMagic);
+#pragma unroll
+          for (int i = 0; i < 2 * kKPT; ++i) {
+            const float nn = t8[i] - kMagic;
+            r8[i] = fmaf(-nn, kPiB, fmaf(-nn, kPiA, x[i]));
+          }
+#pragma unroll
+          for (int i = 0; i < 2 * kKPT; ++i)
+            r8[i] = __uint_as_float(__float_as_uint(r8[i]) + (__float_as_uint(t8[i]) << 31));
+#pragma unroll
+          for (int i = 0; i < 2 * kKPT; ++i) {
+            const float r2 = r8[i] * r8[i];
+            float q = fmaf(kS9, r2, kS7);
+            q = fmaf(q, r2, kS5);
+            q = fmaf(q, r2, kS3);
+            q8[i] = fmaf(q, r2, 1.0f);
+          }
+#pragma unroll
+          for (int c = 0; c < kKPT; ++c) {
+            acc[c] = fmaf(r8[c] * p.y, q8[c], acc[c]);
+            acc2[c] = fmaf(r8[kKPT + c] * p1.y, q8[kKPT + c], acc2[c]);
           }
         }
         if (j < j1) {
