@@ -41,6 +41,21 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
   const int bl = tid % kBS, c = tid / kBS;
   const int b = b0 + bl;
   const int KLr = H / kKC;  // this thread's k range [c*KLr, (c+1)*KLr), a multiple of 4
+  // the gate epilogue's operands, loaded up front so their latency hides under the dot products
+  const int eu = tid / kBS, ebb = tid - eu * kBS;
+  const int ebi = b0 + ebb, ej = j0 + eu;
+  const bool epi = tid < kHS * kBS && ebi < B;
+  float ex_r = 0.f, ex_z = 0.f, ex_n = 0.f, eb_r = 0.f, eb_z = 0.f, eb_n = 0.f, ehp = 0.f;
+  if (epi) {
+    const float* xr = xp + (int64_t)ebi * xp_ld;
+    ex_r = xr[ej];
+    ex_z = xr[H + ej];
+    ex_n = xr[2 * H + ej];
+    eb_r = b_hh[ej];
+    eb_z = b_hh[H + ej];
+    eb_n = b_hh[2 * H + ej];
+    ehp = h_prev ? h_prev[(int64_t)ebi * hp_ld + ej] : 0.0f;
+  }
   const bool hv_ok = h_prev && b < B;
   const float* hrow = h_prev + (int64_t)(hv_ok ? b : 0) * hp_ld + c * KLr;
   float acc[R];
@@ -77,30 +92,25 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
 #pragma unroll
   for (int r = 0; r < R; ++r) part[(c * R + r) * kBS + bl] = acc[r];
   __syncthreads();
-  // gates for kHS units x kBS batch rows (128 items on 256 threads)
-  if (tid < kHS * kBS) {
-    const int u = tid / kBS, bb = tid - u * kBS;
-    const int bi = b0 + bb, j = j0 + u;
-    if (bi < B) {
-      float hr = 0.f, hz = 0.f, hn = 0.f;
-      for (int cc = 0; cc < kKC; ++cc) {
-        hr += part[(cc * R + 0 * kHS + u) * kBS + bb];
-        hz += part[(cc * R + 1 * kHS + u) * kBS + bb];
-        hn += part[(cc * R + 2 * kHS + u) * kBS + bb];
-      }
-      const float* xr = xp + (int64_t)bi * xp_ld;
-      const float r = sigmoidf_(xr[j] + (hr + b_hh[j]));
-      const float z = sigmoidf_(xr[H + j] + (hz + b_hh[H + j]));
-      const float n = tanhf(xr[2 * H + j] + r * (hn + b_hh[2 * H + j]));
-      const float hp = h_prev ? h_prev[(int64_t)bi * hp_ld + j] : 0.0f;
-      h_out[(int64_t)bi * ho_ld + j] = (1.0f - z) * n + z * hp;
-      if (save) {  // training: r, z, n and W_hn h + b_hn of this step, [4][B, T, H] (same row layout as h_out)
-        float* sv = save + (int64_t)bi * ho_ld + j;
-        sv[0] = r;
-        sv[save_plane] = z;
-        sv[2 * save_plane] = n;
-        sv[3 * save_plane] = hn + b_hh[2 * H + j];
-      }
+  // gates for kHS units x kBS batch rows (128 items)
+  if (epi) {
+    const int u = eu, bb = ebb;
+    float hr = 0.f, hz = 0.f, hn = 0.f;
+    for (int cc = 0; cc < kKC; ++cc) {
+      hr += part[(cc * R + 0 * kHS + u) * kBS + bb];
+      hz += part[(cc * R + 1 * kHS + u) * kBS + bb];
+      hn += part[(cc * R + 2 * kHS + u) * kBS + bb];
+    }
+    const float r = sigmoidf_(ex_r + (hr + eb_r));
+    const float z = sigmoidf_(ex_z + (hz + eb_z));
+    const float n = tanhf(ex_n + r * (hn + eb_n));
+    h_out[(int64_t)ebi * ho_ld + ej] = (1.0f - z) * n + z * ehp;
+    if (save) {  // training: r, z, n and W_hn h + b_hn of this step, [4][B, T, H] (same row layout as h_out)
+      float* sv = save + (int64_t)ebi * ho_ld + ej;
+      sv[0] = r;
+      sv[save_plane] = z;
+      sv[2 * save_plane] = n;
+      sv[3 * save_plane] = hn + eb_n;
     }
   }
 }
@@ -118,10 +128,9 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
 // finds dG_{t-1} ready.
 
 // the elementwise part at step t for element (b, j), given the total dh: writes dxp, dGn
-__device__ __forceinline__ void gru_bwd_elem(const float* __restrict__ save, int64_t plane, int64_t idx, float hprev,
-                                             float dh, float* __restrict__ dxp, int64_t xi, int H,
-                                             float* __restrict__ dgn) {
-  const float r = save[idx], z = save[plane + idx], n = save[2 * plane + idx], hn = save[3 * plane + idx];
+__device__ __forceinline__ void gru_bwd_elem_v(float r, float z, float n, float hn, int64_t idx, float hprev,
+                                               float dh, float* __restrict__ dxp, int64_t xi, int H,
+                                               float* __restrict__ dgn) {
   const float dn = dh * (1.0f - z);
   const float dz = dh * (hprev - n);
   const float dan = dn * (1.0f - n * n);
@@ -131,6 +140,13 @@ __device__ __forceinline__ void gru_bwd_elem(const float* __restrict__ save, int
   dxp[xi + H] = daz;
   dxp[xi + 2 * H] = dan;
   dgn[idx] = dan * r;
+}
+
+__device__ __forceinline__ void gru_bwd_elem(const float* __restrict__ save, int64_t plane, int64_t idx, float hprev,
+                                             float dh, float* __restrict__ dxp, int64_t xi, int H,
+                                             float* __restrict__ dgn) {
+  gru_bwd_elem_v(save[idx], save[plane + idx], save[2 * plane + idx], save[3 * plane + idx], idx, hprev, dh, dxp, xi,
+                 H, dgn);
 }
 
 // WT[i][k] = W_hh[k][i] (H x 3H), so the backward's per-unit columns are contiguous rows; 32x32 tiles
@@ -180,11 +196,29 @@ __global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
   const int bl = tid % kBS, c = tid / kBS;
   const int b = b0 + bl;
   const int KLr = K / kKC;  // this thread's reduction range (K % (4 kKC) == 0)
-  // dG_t row of this batch element: (dxp_r, dxp_z) = dG_r, dG_z; dG_n = dgn
+  // the epilogue's operands (this step's z and dh, step t-1's saved gates, dout and h_{t-2}),
+  // loaded up front so their latency hides under the transposed product
+  const int eu = tid / kBS, ebb = tid - eu * kBS;
+  const int ebi = b0 + ebb, ei = i0 + eu;
+  const bool epi = tid < kHS * kBS && ebi < B;
+  const int64_t ee = (int64_t)ebi * H + ei;
+  const int64_t eidx_t = ((int64_t)ebi * T + t) * H + ei, eidx = eidx_t - H;
+  float e_dh = 0.f, e_z = 0.f, e_dout = 0.f, e_hprev = 0.f, s_r = 0.f, s_z = 0.f, s_n = 0.f, s_hn = 0.f;
+  if (epi) {
+    e_dh = dh_in[ee];
+    e_z = save[plane + eidx_t];
+    if (t > 0) {
+      e_dout = dout ? dout[eidx] : 0.0f;
+      e_hprev = t >= 2 ? out[eidx - H] : (h0 ? h0[ee] : 0.0f);
+      s_r = save[eidx];
+      s_z = save[plane + eidx];
+      s_n = save[2 * plane + eidx];
+      s_hn = save[3 * plane + eidx];
+    }
+  }
   float acc[kHS];
 #pragma unroll
   for (int u = 0; u < kHS; ++u) acc[u] = 0.0f;
-  // rows i0..i0+kHS of W_hh^T (contiguous), stored interleaved [k][u] for float4 reads
   for (int e = tid; e < kHS * K / 4; e += kNT) {
     const int u = e / (K / 4), k = 4 * (e - u * (K / 4));
     const float4 v = *reinterpret_cast<const float4*>(w_t + (int64_t)(i0 + u) * K + k);
@@ -227,25 +261,17 @@ __global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
 #pragma unroll
   for (int u = 0; u < kHS; ++u) part[(c * kHS + u) * kBS + bl] = acc[u];
   __syncthreads();
-  if (tid < kHS * kBS) {
-    const int u = tid / kBS, bb = tid - u * kBS;
-    const int bi = b0 + bb, i = i0 + u;
-    if (bi < B) {
-      float s = 0.0f;
-      for (int cc = 0; cc < kKC; ++cc) s += part[(cc * kHS + u) * kBS + bb];
-      const int64_t e = (int64_t)bi * H + i;
-      const int64_t idx_t = ((int64_t)bi * T + t) * H + i;
-      // dh_{t-1} = dh_t z_t + W_hh^T dG_t + dout_{t-1}
-      float dh = dh_in[e] * save[plane + idx_t] + s;
-      if (t == 0) {
-        if (dh0) dh0[e] = dh;
-      } else {
-        const int64_t idx = idx_t - H;  // step t-1
-        if (dout) dh += dout[idx];
-        dh_outbuf[e] = dh;
-        const float hprev = t >= 2 ? out[idx - H] : (h0 ? h0[e] : 0.0f);
-        gru_bwd_elem(save, plane, idx, hprev, dh, dxp, ((int64_t)bi * T + (t - 1)) * 3 * H + i, H, dgn);
-      }
+  if (epi) {
+    float s = 0.0f;
+    for (int cc = 0; cc < kKC; ++cc) s += part[(cc * kHS + eu) * kBS + ebb];
+    // dh_{t-1} = dh_t z_t + W_hh^T dG_t + dout_{t-1}
+    float dh = e_dh * e_z + s;
+    if (t == 0) {
+      if (dh0) dh0[ee] = dh;
+    } else {
+      dh += e_dout;
+      dh_outbuf[ee] = dh;
+      gru_bwd_elem_v(s_r, s_z, s_n, s_hn, eidx, e_hprev, dh, dxp, ((int64_t)ebi * T + (t - 1)) * 3 * H + ei, H, dgn);
     }
   }
 }
