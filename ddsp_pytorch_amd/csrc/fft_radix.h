@@ -131,19 +131,27 @@ __device__ __forceinline__ void dft8(float2& a0, float2& a1, float2& a2, float2&
   a7 = make_float2(e3.x - o3.x, e3.y - o3.y);
 }
 
-template <int N, bool INV>
+template <int N, bool INV, bool SYNC_ENTRY = true>
 __device__ __forceinline__ void fft_n(float2 (&v)[16], float2* lds, int t) {
   static_assert(N >= 16 && N <= 4096 && (N & (N - 1)) == 0, "power-of-two N in [16, 4096]");
   constexpr int Q = N / 16;  // threads per transform
   constexpr int R = (N == 16 || N == 256 || N == 4096) ? 1 : (N == 32 || N == 512) ? 2 : (N == 64 || N == 1024) ? 4 : 8;
   constexpr int A = (N == 16 || N == 32 || N == 64 || N == 128) ? 1 : (N <= 2048 ? 2 : 3);  // radix-16 passes
+  // the twiddles of passes 1.. are loaded up front, so their latency hides behind pass 0
+  Tw4 tw[A > 1 ? A - 1 : 1];
+#pragma unroll
+  for (int pass = 1; pass < A; ++pass) {
+    const int ns = 1 << (4 * pass);
+    tw[pass - 1] = load_tw<INV>((t % ns) * (256 / ns));
+  }
   int Ns = 1;
 #pragma unroll
   for (int pass = 0; pass < A; ++pass) {
-    if (pass > 0) apply_tw(v, load_tw<INV>((t % Ns) * (256 / Ns)));
+    if (pass > 0) apply_tw(v, tw[pass - 1]);
     dft16<INV>(v);
     if (pass == A - 1 && R == 1) return;  // last pass with Ns = N/16: natural order in registers
-    __syncthreads();
+    // (SYNC_ENTRY = false: the caller guarantees no thread still reads lds on entry)
+    if (pass > 0 || SYNC_ENTRY) __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) lds[lds_idx(out_index(t, Ns, r))] = v[r];
     __syncthreads();

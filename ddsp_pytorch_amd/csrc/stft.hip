@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) stft_mag_kernel(const float* __restrict__
   const float* xr = x + (int64_t)b * T;
   float2 v[16];
   load_frames<N>(xr, T, hop, frames, fa, t, v);
-  fft_n<N, false>(v, lds, t);
+  fft_n<N, false, false>(v, lds, t);  // lds untouched so far
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) lds[lds_idx(t + Q * r)] = v[r];
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(256) stft_mag_backward_kernel(const float* __r
   const float* xr = x + (int64_t)b * T;
   float2 v[16];
   load_frames<N>(xr, T, hop, frames, fa, t, v);
-  fft_n<N, false>(v, lds, t);
+  fft_n<N, false, false>(v, lds, t);  // lds untouched so far
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) lds[lds_idx(t + Q * r)] = v[r];

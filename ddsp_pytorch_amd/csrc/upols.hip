@@ -57,6 +57,15 @@ __device__ __forceinline__ void fft4096(float2 (&v)[16], float2* lds) {
   dft16<INV>(v);  // Ns = 256: output index == j + 256 r (coalesced)
 }
 
+// Complex multiply-accumulate as two packed FMAs (v_pk_fma_f32: two fp32 FMAs per lane per
+// instruction): acc += a * b = a.x * (b.x, b.y) + a.y * (-b.y, b.x), with b and its rotation
+// formed once per partition and shared by every accumulator.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
+  acc = __builtin_elementwise_fma((v2f){a.x, a.x}, b, acc);
+  acc = __builtin_elementwise_fma((v2f){a.y, a.y}, b_rot, acc);
+}
+
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
   if (pairing) {
@@ -134,10 +143,11 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
   const float2* Xp = X + (int64_t)pair * nb * kN + f;
   const float2* Hp = Hs + (int64_t)pair * h_pair_stride + f;
   const float2 zero = make_float2(0.f, 0.f);
-  float2 acc[BLK], win[BLK];
+  float2 win[BLK];
+  v2f acc[BLK];
 #pragma unroll
   for (int d = 0; d < BLK; ++d) {
-    acc[d] = zero;
+    acc[d] = (v2f){0.f, 0.f};
     // clamped load + value select (a select of pointers made hipcc go through scratch)
     const float2 xv = Xp[(int64_t)min(b0 + d, nb - 1) * kN];
     win[d] = b0 + d < nb ? xv : zero;
@@ -146,11 +156,9 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
 #pragma unroll 4
   for (int p = 0; p < pmax; ++p) {
     const float2 h = Hp[(int64_t)p * kN];
+    const v2f hb = {h.x, h.y}, hr = {-h.y, h.x};
 #pragma unroll
-    for (int d = 0; d < BLK; ++d) {
-      acc[d].x = fmaf(win[d].x, h.x, fmaf(-win[d].y, h.y, acc[d].x));
-      acc[d].y = fmaf(win[d].x, h.y, fmaf(win[d].y, h.x, acc[d].y));
-    }
+    for (int d = 0; d < BLK; ++d) cmac(acc[d], win[d], hb, hr);
 #pragma unroll
     for (int d = BLK - 1; d > 0; --d) win[d] = win[d - 1];
     const int bn = b0 - p - 1;
@@ -160,7 +168,7 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
   float2* Yp = Y + (int64_t)pair * nb * kN + f;
 #pragma unroll
   for (int d = 0; d < BLK; ++d)
-    if (b0 + d < nb) Yp[(int64_t)(b0 + d) * kN] = acc[d];
+    if (b0 + d < nb) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
 }
 
 // y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
@@ -212,9 +220,9 @@ __global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restric
   const int p0 = blockIdx.y * PC;
   const int grp = blockIdx.z;
   const float2 zero = make_float2(0.f, 0.f);
-  float2 acc[PC];
+  v2f acc[PC];
 #pragma unroll
-  for (int d = 0; d < PC; ++d) acc[d] = zero;
+  for (int d = 0; d < PC; ++d) acc[d] = (v2f){0.f, 0.f};
   const int pr0 = grp * pairs_per_group, pr1 = min(npairs, pr0 + pairs_per_group);
   for (int pair = pr0; pair < pr1; ++pair) {
     const float2* Xp = Xz + (int64_t)pair * nb * kN + f;
@@ -228,16 +236,14 @@ __global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restric
       const float2 xv = Xp[(int64_t)(k - p0) * kN];
       win[0] = make_float2(xv.x, -xv.y);
       const float2 g = Gp[(int64_t)k * kN];
+      const v2f gb = {g.x, g.y}, gr = {-g.y, g.x};
 #pragma unroll
-      for (int d = 0; d < PC; ++d) {
-        acc[d].x = fmaf(win[d].x, g.x, fmaf(-win[d].y, g.y, acc[d].x));
-        acc[d].y = fmaf(win[d].x, g.y, fmaf(win[d].y, g.x, acc[d].y));
-      }
+      for (int d = 0; d < PC; ++d) cmac(acc[d], win[d], gb, gr);
     }
   }
 #pragma unroll
   for (int d = 0; d < PC; ++d)
-    if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = acc[d];
+    if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = make_float2(acc[d].x, acc[d].y);
 }
 
 // T_j = sum_p conj(H_p) GZ_{j+p} for BLK+1 consecutive j, then V_j = T_j + (-1)^f T_{j+1} for the
@@ -252,10 +258,11 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __rest
   const float2* Gp = G + (int64_t)pair * nb * kN + f;
   const float2* Hp = Hs + f;
   const float2 zero = make_float2(0.f, 0.f);
-  float2 acc[BLK + 1], win[BLK + 1];
+  float2 win[BLK + 1];
+  v2f acc[BLK + 1];
 #pragma unroll
   for (int d = 0; d <= BLK; ++d) {
-    acc[d] = zero;
+    acc[d] = (v2f){0.f, 0.f};
     const float2 gv = Gp[(int64_t)min(j0 + d, nb - 1) * kN];
     win[d] = j0 + d < nb ? gv : zero;  // win[d] = GZ_{j0+d+p}
   }
@@ -263,11 +270,9 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __rest
 #pragma unroll 4
   for (int p = 0; p < pmax; ++p) {
     const float2 h = Hp[(int64_t)p * kN];
+    const v2f hc = {h.x, -h.y}, hcr = {h.y, h.x};  // conj(h) and its rotation
 #pragma unroll
-    for (int d = 0; d <= BLK; ++d) {  // conj(h) * win
-      acc[d].x = fmaf(win[d].x, h.x, fmaf(win[d].y, h.y, acc[d].x));
-      acc[d].y = fmaf(win[d].y, h.x, fmaf(-win[d].x, h.y, acc[d].y));
-    }
+    for (int d = 0; d <= BLK; ++d) cmac(acc[d], win[d], hc, hcr);
 #pragma unroll
     for (int d = 0; d < BLK; ++d) win[d] = win[d + 1];
     const int kn = j0 + BLK + p + 1;
