@@ -85,12 +85,18 @@ __global__ void __launch_bounds__(64) impulse_backward_finish_kernel(const doubl
                                                                      const float* __restrict__ wet,
                                                                      float* __restrict__ d_decay,
                                                                      float* __restrict__ d_wet) {
-  if (threadIdx.x != 0) return;
+  // one wave: strided loads in flight together, then a fixed shuffle tree (deterministic)
   double aw = 0.0, ad = 0.0;
-  for (int i = 0; i < nblk; ++i) {
+  for (int i = threadIdx.x; i < nblk; i += 64) {
     aw += partials[2 * i];
     ad += partials[2 * i + 1];
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    aw += __shfl_down(aw, o, 64);
+    ad += __shfl_down(ad, o, 64);
+  }
+  if (threadIdx.x != 0) return;
   const float d = -decay[0];
   const float spg = d > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-d));  // softplus'(d)
   const float w = 1.0f / (1.0f + expf(-wet[0]));

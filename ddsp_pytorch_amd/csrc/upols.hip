@@ -138,7 +138,9 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
                                                         int64_t h_pair_stride, int nb, int Q,
                                                         float2* __restrict__ Y) {
   const int f = blockIdx.x * kNT + threadIdx.x;
-  const int b0 = blockIdx.y * BLK;
+  // chunks end-aligned: the partial chunk is the first one, whose blocks see the fewest
+  // partitions (min(Q, b0 + BLK) iterations), instead of a nearly empty last chunk paying Q
+  const int b0 = nb - (int)(gridDim.y - blockIdx.y) * BLK;
   const int pair = blockIdx.z;
   const float2* Xp = X + (int64_t)pair * nb * kN + f;
   const float2* Hp = Hs + (int64_t)pair * h_pair_stride + f;
@@ -149,8 +151,8 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
   for (int d = 0; d < BLK; ++d) {
     acc[d] = (v2f){0.f, 0.f};
     // clamped load + value select (a select of pointers made hipcc go through scratch)
-    const float2 xv = Xp[(int64_t)min(b0 + d, nb - 1) * kN];
-    win[d] = b0 + d < nb ? xv : zero;
+    const float2 xv = Xp[(int64_t)max(b0 + d, 0) * kN];
+    win[d] = b0 + d >= 0 ? xv : zero;
   }
   const int pmax = min(Q, b0 + BLK);
 #pragma unroll 4
@@ -168,7 +170,7 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
   float2* Yp = Y + (int64_t)pair * nb * kN + f;
 #pragma unroll
   for (int d = 0; d < BLK; ++d)
-    if (b0 + d < nb) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
+    if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
 }
 
 // y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
@@ -209,27 +211,33 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
 // For a packed pair (z = x_a + i x_b, g likewise) the real part of F^-1(conj(X) GZ) is corr_a + corr_b:
 // the packed spectra are used as they are.  GZ is shared by both gradients, and X is the forward's.
 
-// dH_p[f] = sum_{pair in group} sum_j conj(X[pair][j][f]) * G[pair][j+p][f]: one bin per thread, PC
-// consecutive partitions with a sliding register window of conj(X); grid (N/256, ceil(Q/PC), groups).
+// dH_p[f] = sum_{pair in group} sum_j conj(X[pair][j][f]) * G[pair][j+p][f]: PC consecutive
+// partitions per thread with a sliding register window of conj(X).  A workgroup is 64 bins x
+// kCorrSlices waves; the waves take interleaved pairs of the group (pair = grp * S + s, stepping
+// by groups * S) and are summed through LDS, so the grid has (N/64) * ceil(Q/PC) * groups
+// workgroups and only `groups` partial spectra per partition reach HBM.
+constexpr int kCorrSlices = 4;
 template <int PC>
-__global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restrict__ Xz,
-                                                         const float2* __restrict__ Gw, int nb, int Q,
-                                                         int npairs, int pairs_per_group,
-                                                         float2* __restrict__ part) {
-  const int f = blockIdx.x * kNT + threadIdx.x;
+__global__ void __launch_bounds__(64 * kCorrSlices) upols_corr_kernel(const float2* __restrict__ Xz,
+                                                                     const float2* __restrict__ Gw, int nb,
+                                                                     int Q, int npairs, int groups,
+                                                                     float2* __restrict__ part) {
+  __shared__ float2 red[kCorrSlices][PC][64];
+  const int lane = threadIdx.x & 63, s = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
   const int p0 = blockIdx.y * PC;
   const int grp = blockIdx.z;
   const float2 zero = make_float2(0.f, 0.f);
   v2f acc[PC];
 #pragma unroll
   for (int d = 0; d < PC; ++d) acc[d] = (v2f){0.f, 0.f};
-  const int pr0 = grp * pairs_per_group, pr1 = min(npairs, pr0 + pairs_per_group);
-  for (int pair = pr0; pair < pr1; ++pair) {
+  for (int pair = grp * kCorrSlices + s; pair < npairs; pair += groups * kCorrSlices) {
     const float2* Xp = Xz + (int64_t)pair * nb * kN + f;
     const float2* Gp = Gw + (int64_t)pair * nb * kN + f;
     float2 win[PC];
 #pragma unroll
     for (int d = 0; d < PC; ++d) win[d] = zero;
+#pragma unroll 4
     for (int k = p0; k < nb; ++k) {
 #pragma unroll
       for (int d = PC - 1; d > 0; --d) win[d] = win[d - 1];
@@ -242,8 +250,18 @@ __global__ void __launch_bounds__(kNT) upols_corr_kernel(const float2* __restric
     }
   }
 #pragma unroll
-  for (int d = 0; d < PC; ++d)
-    if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = make_float2(acc[d].x, acc[d].y);
+  for (int d = 0; d < PC; ++d) red[s][d][lane] = make_float2(acc[d].x, acc[d].y);
+  __syncthreads();
+  // wave s reduces partitions d = s, s + S, ... over the slices (fixed order: deterministic)
+  for (int d = s; d < PC; d += kCorrSlices) {
+    float2 t = red[0][d][lane];
+#pragma unroll
+    for (int q = 1; q < kCorrSlices; ++q) {
+      t.x += red[q][d][lane].x;
+      t.y += red[q][d][lane].y;
+    }
+    if (p0 + d < Q) part[((int64_t)grp * Q + p0 + d) * kN + f] = t;
+  }
 }
 
 // T_j = sum_p conj(H_p) GZ_{j+p} for BLK+1 consecutive j, then V_j = T_j + (-1)^f T_{j+1} for the
@@ -317,6 +335,11 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace
 
+// IR-gradient partial sums: one per group of kCorrSlices pairs, at most 8
+static int64_t corr_groups(int64_t npairs) {
+  return std::min<int64_t>((npairs + kCorrSlices - 1) / kCorrSlices, 8);
+}
+
 int64_t upols_partitions(int64_t klen) { return (std::max<int64_t>(klen, 1) + kP - 1) / kP; }
 int64_t upols_blocks(int64_t n) { return (n + kP - 1) / kP; }
 
@@ -371,7 +394,7 @@ size_t upols_spectra_bytes(int64_t rows, int64_t n) {
 
 size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x) {
   const int64_t Q = upols_partitions(std::min(klen, n));
-  const int64_t groups = std::min<int64_t>((rows + 1) / 2, 16);
+  const int64_t groups = corr_groups((rows + 1) / 2);
   return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)groups * Q * kN * sizeof(float2);
 }
 
@@ -381,8 +404,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   const int64_t nb = upols_blocks(n);
   const int64_t kc = std::min(klen, n);
   const int64_t Q = upols_partitions(kc);
-  const int64_t groups = std::min<int64_t>(npairs, 16);
-  const int64_t ppg = (npairs + groups - 1) / groups;
+  const int64_t groups = corr_groups(npairs);
   const bool need_x = dimp && !x_spectra;
   if (!ws || ws_bytes < upols_backward_workspace_bytes(rows, n, klen, !need_x)) return DDSP_HIP_EWORKSPACE;
   if (nb > INT32_MAX || npairs > 65535 || Q > 65535 || (nb + 15) / 16 > 65535) return DDSP_HIP_EINVAL;
@@ -413,8 +435,9 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
                          n, (int)rows, 1, (int)nb, -1, 0, 0, Xs);
       if ((st = launch_status())) return st;
     }
-    hipLaunchKernelGGL(upols_corr_kernel<16>, dim3(kN / kNT, (unsigned)((Q + 15) / 16), (unsigned)groups),
-                       dim3(kNT), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)ppg, part);
+    hipLaunchKernelGGL(upols_corr_kernel<8>, dim3(kN / 64, (unsigned)((Q + 7) / 8), (unsigned)groups),
+                       dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
+                       part);
     if ((st = launch_status())) return st;
     hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Q), dim3(kNT), 0, S(stream), part, (int)groups,
                        (int)Q, kc, dimp);
