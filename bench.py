@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--noise", choices=("device", "inject"), default="device")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-op-leg", action="store_true")
+    p.add_argument("--chunks", type=int, default=4,
+                   help="N>1 scatter/gather leg: batch chunks pipelined through the collectives")
     p.add_argument("--no-gather", action="store_true",
                    help="N>1: skip the synth + RCCL gather-to-rank-0 leg (reported separately as "
                         "'gathered'; value is always the left-sharded throughput)")
@@ -431,6 +433,36 @@ def main():
                               "unit": "samples/s", "collective": "torch.distributed.gather (RCCL)",
                               "ms_per_step": round(float(tt.item()) / args.steps * 1e3, 4)}
         del g
+        # root-held batch: controls scattered from rank 0 in chunks, audio gathered back,
+        # scatter(i+1) || synth(i) || gather(i-1) (shard.synthesize_pipelined); IR broadcast once
+        from ddsp_pytorch_amd.shard import broadcast_module, synthesize_pipelined
+        if syn.reverb is not None:
+            broadcast_module(syn.reverb)
+        keys = ["f0", "param", "mags"] + (["noise"] if args.noise == "inject" else [])
+        tails = [tuple(inp[k].shape[1:]) for k in keys]
+        held = None
+        if rank == 0:
+            full = make_inputs(B * world, F, H, NB, bs, seed=0, device=dev,
+                               with_noise=(args.noise == "inject"))
+            held = [full[k] for k in keys]
+        pipe = lambda: synthesize_pipelined(syn, held, B * world, tails, chunks=args.chunks, device=dev)
+        for _ in range(2):
+            pipe()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            g = pipe()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tp = time.perf_counter() - tp
+        tt = torch.tensor([tp], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        result["scatter_gather"] = {
+            "value": round(samples_per_step * args.steps / float(tt.item()), 1), "unit": "samples/s",
+            "ms_per_step": round(float(tt.item()) / args.steps * 1e3, 4), "chunks": args.chunks,
+            "collective": "torch.distributed scatter (controls) + gather (audio), RCCL, async per chunk"}
+        del g, held
 
     if rank == 0 and not args.no_op_leg:
         # op-boundary oscillator (core.py:136): per-sample inputs materialised in HBM

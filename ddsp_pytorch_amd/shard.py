@@ -57,3 +57,121 @@ def synthesize_sharded(synth, inputs, rank, world, gather=False, dst=0):
     if gather:
         return gather_audio(audio, batch, dst=dst)
     return audio
+
+
+# ---------------------------------------------------------------------------------------------
+# Root-held batches: the frame-rate controls live on one rank, which scatters
+# them, every rank synthesises its shard, and the audio is gathered back.  The reverb IR is
+# broadcast once.  The batch is cut into chunks so the collectives of one chunk overlap the
+# synthesis of its neighbours: scatter(i+1) || synth(i) || gather(i-1).  With RCCL the
+# collectives run on the process group's own HIP stream and the synthesis on the current one;
+# async work handles order them (wait() makes the current stream wait, without a host sync).
+# ---------------------------------------------------------------------------------------------
+
+
+def broadcast_module(module, src=0, group=None):
+    """Broadcast a module's parameters and buffers (the reverb IR parameters) from ``src``.
+
+    Each tensor is received into a copy and written back with copy_ so its version counter
+    moves and caches keyed on it (Reverb's IR spectrum) are invalidated."""
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            tmp = t.detach().clone()
+            dist.broadcast(tmp, src, group=group)
+            t.copy_(tmp)
+
+
+def pack_items(tensors):
+    """[b, ...] tensors -> one [b, sum of per-item sizes] buffer (a single collective per chunk)."""
+    b = tensors[0].shape[0]
+    return torch.cat([t.reshape(b, -1) for t in tensors], 1)
+
+
+def unpack_items(packed, tails):
+    """Inverse of pack_items for per-item shapes ``tails``."""
+    out, o = [], 0
+    for tail in tails:
+        n = 1
+        for d in tail:
+            n *= int(d)
+        out.append(packed[:, o:o + n].reshape((packed.shape[0],) + tuple(tail)))
+        o += n
+    return out
+
+
+def _scatter_async(full, batch, width_cols, dtype, device, src, group):
+    """Start scattering [batch, width_cols] (significant on src only) into ragged shards."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = [shard_range(batch, r, world) for r in range(world)]
+    width = max(b - a for a, b in sizes)
+    recv = torch.empty((width, width_cols), dtype=dtype, device=device)
+    send = None
+    if rank == src:
+        send = []
+        for a, b in sizes:
+            part = full[a:b]
+            if b - a < width:
+                part = torch.cat([part, part.new_zeros((width - (b - a), width_cols))], 0)
+            send.append(part.contiguous())
+    work = dist.scatter(recv, send, src=src, group=group, async_op=True)
+    a, b = sizes[rank]
+    return work, recv, b - a
+
+
+def _gather_async(local, batch, dst, group):
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = [shard_range(batch, r, world) for r in range(world)]
+    width = max(b - a for a, b in sizes)
+    send = local
+    if local.shape[0] < width:
+        send = torch.cat([local, local.new_zeros((width - local.shape[0],) + tuple(local.shape[1:]))], 0)
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    work = dist.gather(send.contiguous(), recv, dst=dst, group=group, async_op=True)
+    return work, recv, sizes
+
+
+def chunk_bounds(batch, chunks):
+    """[start, stop) of each of ``chunks`` near-equal pieces of the global batch (empty ones dropped)."""
+    chunks = max(1, min(int(chunks), int(batch)))
+    return [r for r in (shard_range(batch, c, chunks) for c in range(chunks)) if r[1] > r[0]]
+
+
+def synthesize_pipelined(synth, inputs, batch, tails, chunks=4, src=0, dst=0, group=None,
+                         device=None, dtype=torch.float32):
+    """Root-held batch through the sharded synth path with overlapped collectives.
+
+    inputs: list of full-batch [batch, *tail] tensors on ``src`` (ignored elsewhere, may be
+    None), in the order ``synth`` takes them; tails: their per-item shapes (every rank knows
+    them).  Each of ``chunks`` pieces of the batch is scattered over the ranks, synthesised
+    ([b, T, 1] per shard) and gathered on ``dst``.  Returns [batch, T, 1] on dst, None elsewhere.
+    """
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    if batch < world:
+        raise ValueError(f"batch {batch} smaller than the world size {world}")
+    bounds = chunk_bounds(batch, min(int(chunks), batch // world))  # every shard non-empty
+    cols = sum(int(torch.Size(t).numel()) for t in tails)
+    packed = pack_items(inputs) if rank == src else None
+
+    def start(c):
+        a, b = bounds[c]
+        return _scatter_async(packed[a:b] if packed is not None else None, b - a, cols, dtype,
+                              device, src, group)
+
+    pending = start(0)
+    gathers = []
+    for c in range(len(bounds)):
+        work, recv, n = pending
+        work.wait()
+        if c + 1 < len(bounds):
+            pending = start(c + 1)  # in flight while this chunk is synthesised
+        audio = synth(*unpack_items(recv[:n], tails))
+        gathers.append(_gather_async(audio, bounds[c][1] - bounds[c][0], dst, group))
+    out = []
+    for work, recv, sizes in gathers:
+        work.wait()
+        if rank == dst:
+            out.append(torch.cat([r[: b - a] for r, (a, b) in zip(recv, sizes)], 0))
+    return torch.cat(out, 0) if rank == dst else None
