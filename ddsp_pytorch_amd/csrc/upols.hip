@@ -377,8 +377,6 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   if (st) return st;
   const int64_t h_stride = per_row_kernel ? upols_partitions(klen) * kN : 0;
   // 16 output blocks per thread: each X row is re-read (Q+15)/16 times through L2
-  // (an LDS-tiled variant that reads X once measured 25% slower: lower occupancy, exposed loads)
-  // 16 output blocks per thread: each X row is re-read (Q+15)/16 times through L2
   // (measured slower: an LDS-tiled variant that reads X once, 25%: lower occupancy, exposed
   // loads; every operand loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one
   // thread per (pair, bin) streaming all blocks with a register ring, 8%)
