@@ -277,6 +277,34 @@ def test_config2_synth_path(dd):
         assert e < PARITY_RMS, (b, e)
 
 
+def test_config2_size_independent_properties(dd):
+    """Full config-2 size, properties the oracle need not run for: (1) the fused synthesis of
+    an item does not depend on the rest of the batch (bit-exact: one workgroup per (item,
+    frame)); (2) the reverb is linear over the whole batch; (3) reversing the batch reverses
+    the output (the UPOLS row pairing swaps real and imaginary roles: fp32 rounding only)."""
+    from ddsp_pytorch_amd.synth import make_inputs
+    inp = make_inputs(64, 200, 100, 65, 512, seed=11, device="cuda")
+    args = (512, 48000)
+    with torch.no_grad():
+        full = dd.core.synth_frames(inp["f0"], inp["param"], inp["mags"], *args, bias=-5.0,
+                                    noise=inp["noise"])
+        for b in (0, 17, 63):
+            sl = slice(b, b + 1)
+            one = dd.core.synth_frames(inp["f0"][sl], inp["param"][sl], inp["mags"][sl], *args,
+                                       bias=-5.0, noise=inp["noise"][sl])
+            assert torch.equal(one, full[sl]), b
+        rv = dd.Reverb(48000, 48000).cuda()
+        x1 = full
+        x2 = torch.randn_like(full) * 0.1
+        y1, y2, y12 = rv(x1), rv(x2), rv(x1 + 0.5 * x2)
+        scale = float(y12.pow(2).mean().sqrt())
+        lin = float((y12 - (y1 + 0.5 * y2)).pow(2).mean().sqrt())
+        assert lin < 1e-6 * scale, (lin, scale)
+        yr = rv(x1.flip(0)).flip(0)
+        d = float((yr - y1).pow(2).mean().sqrt())
+        assert d < 1e-6 * scale, (d, scale)
+
+
 # ------------------------------------------------------------------ fused-controls kernels
 @pytest.mark.parametrize("name", ["g2_controls", "g2_controls_rt"])
 def test_harmonic_params_golden(dd, name):
