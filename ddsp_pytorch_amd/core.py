@@ -399,6 +399,28 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     return (out, harm, nz) if parts else out
 
 
+def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed, bias=-5.0):
+    """synth_frames with on-device noise whose Philox offset is the device word counter[0]
+    (int64, advanced by one on the stream after the launch): for calls replayed from a captured
+    HIP graph, where by-value offsets would freeze.  Call k equals
+    synth_frames(..., noise=None) drawn with (seed, offset=k).  Inference only."""
+    _dev(f0, param, mags)
+    B, F, H1 = param.shape
+    NB = mags.shape[-1]
+    bs = int(block_size)
+    if f0.shape != (B, F, 1) or mags.shape[:2] != (B, F) or H1 < 2:
+        raise RuntimeError("synth_frames_counter: f0 [B,F,1], param [B,F,H+1], mags [B,F,NB] expected")
+    if counter.dtype != torch.int64 or counter.numel() < 1 or counter.device != f0.device:
+        raise RuntimeError("synth_frames_counter: counter must be a device int64 tensor")
+    if not synth_frames_in_envelope(H1 - 1, NB, bs, B):
+        raise RuntimeError("synth_frames_counter: shape outside the fused kernel's envelope")
+    out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=f0.device)
+    _lib.call("synth_frames_counter", _lib.ptr(_c(f0)), _lib.ptr(_c(param)), _lib.ptr(_c(mags)), float(bias),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(counter), _lib.ptr(out), B, F, H1 - 1, NB, bs,
+              float(sample_rate), _lib.stream_of(out))
+    return out
+
+
 def reverb_build_impulse(noise, decay, wet, sample_rate):
     """modules.py:21-26 Reverb.build_impulse: noise[L,1] -> impulse [1, L, 1]."""
     _dev(noise, decay, wet)

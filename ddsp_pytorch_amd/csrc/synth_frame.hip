@@ -25,7 +25,8 @@ template <bool RNG>
 __global__ void __launch_bounds__(256) synth_frame_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
-    float* __restrict__ out, float* __restrict__ harm_out, float* __restrict__ noise_out, int F, int H,
+    const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
+    float* __restrict__ noise_out, int F, int H,
     int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
   extern __shared__ float4 smem4[];
   __shared__ double red[32];
@@ -59,6 +60,11 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   fill_cos_table(ct, n);
   for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
   const int quads = bs >> 2;
+  if (RNG && counter) {  // graph-replayed streams: the Philox offset advances in device memory
+    const uint64_t o = (((uint64_t)off1 << 32) | off0) + *counter;
+    off0 = (uint32_t)o;
+    off1 = (uint32_t)(o >> 32);
+  }
   for (int t = tid; t < quads; t += NT) {
     float4 v;
     if (RNG) {
@@ -165,6 +171,8 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
       make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121
 }
 
+__global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
+
 }  // namespace
 }  // namespace ddsp
 
@@ -172,11 +180,11 @@ using namespace ddsp;
 
 extern "C" {
 
-int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,
-                          const float* noise, uint64_t seed, uint64_t offset, float* out,
-                          float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
-                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
-                          void* stream) {
+static int synth_frames_launch(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                               const float* noise, uint64_t seed, uint64_t offset, uint64_t* counter, float* out,
+                               float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
+                               int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                               void* stream) {
   if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
   if (!f0 || !param || !raw_magnitudes || !out) return DDSP_HIP_EINVAL;
@@ -209,13 +217,32 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
   const dim3 grid((unsigned)frames, (unsigned)batch);
   if (noise)
     hipLaunchKernelGGL(synth_frame_kernel<false>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
-                       bias, noise, k0, k1, o0, o1, out, harmonic_out, noise_out, (int)frames,
+                       bias, noise, k0, k1, o0, o1, nullptr, out, harmonic_out, noise_out, (int)frames,
                        (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
   else
     hipLaunchKernelGGL(synth_frame_kernel<true>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
-                       bias, nullptr, k0, k1, o0, o1, out, harmonic_out, noise_out, (int)frames,
+                       bias, nullptr, k0, k1, o0, o1, counter, out, harmonic_out, noise_out, (int)frames,
                        (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
+  if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
   return launch_status();
+}
+
+int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                          const float* noise, uint64_t seed, uint64_t offset, float* out,
+                          float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
+                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                          void* stream) {
+  return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
+                             noise_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
+}
+
+int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                  uint64_t seed, uint64_t* counter, float* out, int64_t batch, int64_t frames,
+                                  int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                                  void* stream) {
+  if (!counter) return DDSP_HIP_EINVAL;
+  return synth_frames_launch(f0, param, raw_magnitudes, bias, nullptr, seed, 0, counter, out, nullptr, nullptr,
+                             batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,107 @@
+"""Realtime streaming on a captured HIP graph (BASELINE.json config 3).
+
+The reference's realtime host, the `ddsp~` Pd external, calls the exported model once per
+1024-sample buffer from a worker thread (`realtime/ddsp_tilde/ddsp_model.cpp:32-52`,
+`ddsp_tilde.cpp:67-98`): pitch and loudness at audio rate in, audio out, the GRU state carried
+between calls in `cache_gru` (`decoder.py:56-60`), no reverb (`export.py:37-40`).  At batch 1
+and 4 frames per call that forward is ~25 short launches (MLPs, LayerNorms, the GRU steps, the
+synthesis), so its latency is launch-bound, not compute-bound.
+
+`RealtimeGraph` captures one call — loudness normalisation, decimation by block_size, the
+control network with the cached GRU state, the fused synthesis kernel — into a HIP graph
+(`torch.cuda.CUDAGraph` is hipGraph on ROCm) over static device buffers, and replays it per
+call: one graph launch plus the two host<->device copies.  The on-device noise takes its
+Philox offset from a device counter the graph advances (`ddsp_hip_synth_frames_counter`), so
+every replay draws fresh noise; call k equals the eager model run with noise offset k.
+"""
+import torch
+
+from . import core
+from .decoder import gru_decoder_forward
+
+
+class RealtimeGraph:
+    """Graph-replayed realtime forward of a `DDSPDecoder` (the ScriptDDSP realtime model of
+    export.py:23-40: `forward(pitch[1,N,1], loudness[1,N,1]) -> audio[1,N,1]`).
+
+    The model's `decoder.cache_gru` is the stream state (updated in place by every call, as in
+    decoder.py:56-60); `reset()` zeroes it and rewinds the noise counter.  The returned tensor
+    is a static buffer overwritten by the next call (the host copies it out, as `ddsp~` does
+    with memcpy)."""
+
+    def __init__(self, model, call_samples=1024, mean_loudness=0.0, std_loudness=1.0,
+                 seed=0x5EEDDD5B, device=None, warmup=3):
+        device = torch.device(device) if device is not None else next(model.parameters()).device
+        if device.type != "cuda":
+            raise RuntimeError("RealtimeGraph: the model must be on a HIP device")
+        bs = int(model.block_size)
+        N = int(call_samples)
+        if N % bs:
+            raise RuntimeError(f"RealtimeGraph: call_samples {N} must be a multiple of block_size {bs}")
+        if not core.synth_frames_in_envelope(model.harmonic_proj.out_features - 1,
+                                             model.noise_proj.out_features, bs, 1):
+            raise RuntimeError("RealtimeGraph: model shape outside the fused synthesis kernel's envelope")
+        self.model = model
+        self.device = device
+        self.block_size = bs
+        self.call_samples = N
+        self.sample_rate = float(model.sample_rate)
+        self.mean_loudness = float(mean_loudness)
+        self.std_loudness = float(std_loudness)
+        self.seed = int(seed)
+        self.bias = float(model.noise_synth.initial_bias)
+        self.pitch = torch.zeros(1, N, 1, device=device)
+        self.loudness = torch.zeros(1, N, 1, device=device)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+        self._pitch_h = torch.zeros(1, N, 1).pin_memory()
+        self._loud_h = torch.zeros(1, N, 1).pin_memory()
+        self._out_h = torch.zeros(1, N, 1).pin_memory()
+        self.graph = torch.cuda.CUDAGraph()
+        cache0 = model.decoder.cache_gru.detach().clone()
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(max(1, int(warmup))):  # library handles / workspaces before capture
+                self._forward()
+        torch.cuda.current_stream(device).wait_stream(side)
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = self._forward()
+        torch.cuda.synchronize(device)
+        model.decoder.cache_gru.copy_(cache0)
+        self.counter.zero_()
+
+    def _forward(self):
+        """export.py:33-40 realtime ScriptDDSP.forward with the model's synthesis fused."""
+        m, bs = self.model, self.block_size
+        pitch = self.pitch[:, ::bs]
+        loudness = (self.loudness[:, ::bs] - self.mean_loudness) / self.std_loudness
+        hidden = gru_decoder_forward(m.decoder, pitch, loudness, None, realtime=True)
+        param = m.harmonic_proj(hidden)
+        mags = m.noise_proj(hidden)
+        return core.synth_frames_counter(pitch, param, mags, bs, self.sample_rate, self.counter,
+                                         self.seed, bias=self.bias)
+
+    def reset(self):
+        self.model.decoder.cache_gru.zero_()
+        self.counter.zero_()
+
+    @torch.no_grad()
+    def __call__(self, pitch, loudness):
+        """pitch, loudness [1, N, 1] on the host (returns a host tensor) or on the device (returns
+        the device output buffer)."""
+        if tuple(pitch.shape) != (1, self.call_samples, 1) or tuple(loudness.shape) != tuple(pitch.shape):
+            raise RuntimeError(f"RealtimeGraph: pitch and loudness must be [1, {self.call_samples}, 1]")
+        stream = torch.cuda.current_stream(self.device)
+        if pitch.is_cuda:
+            self.pitch.copy_(pitch)
+            self.loudness.copy_(loudness)
+            self.graph.replay()
+            return self.out
+        self._pitch_h.copy_(pitch)
+        self._loud_h.copy_(loudness)
+        self.pitch.copy_(self._pitch_h, non_blocking=True)
+        self.loudness.copy_(self._loud_h, non_blocking=True)
+        self.graph.replay()
+        self._out_h.copy_(self.out, non_blocking=True)
+        stream.synchronize()
+        return self._out_h

@@ -140,6 +140,17 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                           int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                           void* stream);
 
+/* ddsp_hip_synth_frames for a stream of calls replayed from a captured HIP graph (the ddsp~
+ * realtime host, realtime/ddsp_tilde/ddsp_model.cpp:32-52, calling the exported model once per
+ * 1024-sample buffer): the Philox offset of the on-device noise is read from the device word
+ * *counter, which a second launch on the same stream then increments, so every replay draws
+ * fresh noise (a graph freezes by-value arguments).  Call k draws the noise of
+ * ddsp_hip_synth_frames(..., seed, offset = k, ...). */
+int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                  uint64_t seed, uint64_t* counter, float* out, int64_t batch, int64_t frames,
+                                  int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                                  void* stream);
+
 /* modules.py:21-26  Reverb.build_impulse: noise[L]*exp(-softplus(-decay)*t*500)*sigmoid(wet),
  * impulse[0] = 1.  decay and wet are device scalars. */
 int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const float* wet,

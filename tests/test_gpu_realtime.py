@@ -1,0 +1,110 @@
+"""Config 3 realtime stream on a captured HIP graph (ddsp_pytorch_amd.realtime.RealtimeGraph):
+graph replays equal the eager realtime forward call for call (GRU state carried in cache_gru,
+decoder.py:56-60; noise offset = call index), and the harmonic part of every call matches the
+torch-CPU oracle of the reference's harmonic synth (oracle/torch_ref.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rms
+
+gpu = pytest.mark.gpu
+BS, H, NB, N = 256, 64, 65, 1024
+
+
+def _model(hidden=64, seed=0):
+    import ddsp_pytorch_amd as dd
+    torch.manual_seed(seed)
+    m = dd.DDSPDecoder(hidden, H, NB, 48000, BS, False).eval()
+    with torch.no_grad():  # a non-zero initial stream state
+        m.decoder.cache_gru.normal_(0, 0.1)
+    return m
+
+
+def _calls(n, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        pitch = 80.0 * 10.0 ** torch.rand(1, N, 1, generator=g)
+        loud = torch.randn(1, N, 1, generator=g) - 2.0
+        out.append((pitch, loud))
+    return out
+
+
+def _eager(m, pitch, loud, k, seed, mean, std):
+    """export.py:33-40 realtime forward, run eagerly with noise offset k; returns (signal, harmonic,
+    harmonic controls)."""
+    from ddsp_pytorch_amd import core
+    from ddsp_pytorch_amd.decoder import gru_decoder_forward
+    p = pitch[:, ::BS].contiguous()
+    l = (loud[:, ::BS] - mean) / std
+    hidden = gru_decoder_forward(m.decoder, p, l, None, realtime=True)
+    param = m.harmonic_proj(hidden)
+    mags = m.noise_proj(hidden)
+    sig, harm, _ = core._synth_frames_launch(p, param, mags, BS, 48000.0, -5.0, None, True, seed, k)
+    return sig, harm, param, p
+
+
+def test_realtime_graph_needs_device():
+    from ddsp_pytorch_amd.realtime import RealtimeGraph
+    with pytest.raises(RuntimeError):
+        RealtimeGraph(_model())
+
+
+@gpu
+def test_realtime_graph_matches_eager_calls():
+    from ddsp_pytorch_amd.realtime import RealtimeGraph
+    from oracle import torch_ref as tr
+    dev = torch.device("cuda", 0)
+    mean, std, seed = -3.0, 1.5, 77
+    mg = _model().to(dev)
+    me = _model().to(dev)
+    rt = RealtimeGraph(mg, N, mean, std, seed=seed)
+    with torch.no_grad():
+        for k, (pitch, loud) in enumerate(_calls(5)):
+            y = rt(pitch, loud).clone()
+            ye, he, param, p = _eager(me, pitch.to(dev), loud.to(dev), k, seed, mean, std)
+            assert y.shape == (1, N, 1) and not y.is_cuda
+            assert float((y - ye.cpu()).abs().max()) <= 1e-6, k
+            assert torch.allclose(mg.decoder.cache_gru, me.decoder.cache_gru, atol=1e-6)
+            # harmonic part against the oracle (modules.py:44-80 on the CPU)
+            pc = param.cpu()
+            amp, dist = tr.harmonic_controls(pc[..., :1], pc[..., 1:], p.cpu(), 48000)
+            ref = tr.harmonic_forward(amp, dist, p.cpu(), BS, 48000)
+            assert rms(he.cpu().numpy(), ref.numpy()) < 1e-6, k
+
+
+@gpu
+def test_realtime_graph_noise_advances_and_reset():
+    from ddsp_pytorch_amd.realtime import RealtimeGraph
+    dev = torch.device("cuda", 0)
+    m = _model().to(dev)
+    cache0 = m.decoder.cache_gru.clone()
+    rt = RealtimeGraph(m, N)
+    assert torch.equal(m.decoder.cache_gru, cache0)  # capture leaves the stream state untouched
+    pitch, loud = _calls(1)[0]
+    with torch.no_grad():
+        m.decoder.cache_gru.zero_()
+        y0 = rt(pitch, loud).clone()
+        m.decoder.cache_gru.zero_()
+        y1 = rt(pitch, loud).clone()  # same state, next noise offset
+        assert not torch.equal(y0, y1)
+        rt.reset()
+        y2 = rt(pitch, loud).clone()
+    assert torch.equal(y0, y2)
+    assert int(rt.counter.item()) == 1
+    # device inputs return the device output buffer
+    yd = rt(pitch.to(dev), loud.to(dev))
+    assert yd.is_cuda and torch.isfinite(yd).all()
+    assert np.isfinite(y0.numpy()).all()
+
+
+@gpu
+def test_realtime_graph_rejects_bad_shapes():
+    from ddsp_pytorch_amd.realtime import RealtimeGraph
+    dev = torch.device("cuda", 0)
+    with pytest.raises(RuntimeError):
+        RealtimeGraph(_model().to(dev), 1000)  # not a multiple of block_size
+    rt = RealtimeGraph(_model().to(dev), N)
+    with pytest.raises(RuntimeError):
+        rt(torch.zeros(1, 512, 1), torch.zeros(1, 512, 1))
