@@ -21,6 +21,24 @@ _I = ctypes.c_int
 _U64 = ctypes.c_uint64
 _SZ = ctypes.c_size_t
 
+
+
+class DenseInput(ctypes.Structure):
+    """ddsp_hip_dense_input (include/ddsp_hip.h)."""
+    _fields_ = [("x", _P), ("ld", _I64), ("width", _I64), ("scale", _F), ("shift", _F), ("w1", _P),
+                ("b1", _P), ("gamma", _P), ("beta", _P), ("x_copy", _P)]
+
+
+DENSE_MAX_INPUTS = 3
+DENSE_MAX_PROBLEMS = 2
+
+
+class DenseProblem(ctypes.Structure):
+    """ddsp_hip_dense_problem (include/ddsp_hip.h)."""
+    _fields_ = [("inputs", DenseInput * DENSE_MAX_INPUTS), ("n_inputs", _I), ("weight", _P), ("bias", _P),
+                ("y", _P), ("ldy", _I64), ("out_features", _I64)]
+
+
 # name -> (restype, argtypes); must match include/ddsp_hip.h exactly
 SIGNATURES = {
     "ddsp_hip_status_string": (ctypes.c_char_p, [_I]),
@@ -47,6 +65,7 @@ SIGNATURES = {
     "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
     "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P]),
     "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_dense_rows": (_I, [_P, _I, _I64, _P]),
     "ddsp_hip_gru_forward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_gru_backward_workspace_size": (_SZ, [_I64, _I64]),
     "ddsp_hip_gru_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),

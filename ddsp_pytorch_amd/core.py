@@ -13,6 +13,7 @@ Besides the six reference functions, the fused frame-rate ops used by the module
 drop-ins (``modules.py``) live here: ``harmonic_controls``, ``harmonic_synth_frames``,
 ``filtered_noise``, ``reverb_build_impulse``, ``reverb_spectrum``, ``reverb_apply``.
 """
+import ctypes
 import itertools
 import math
 
@@ -490,6 +491,48 @@ def gru(x, gru_module, h0=None):
     _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
               _lib.ptr(h_last), None, B, T, H, _lib.stream_of(out))
     return out, h_last
+
+
+def dense_input(x, width=None, ld=None, scale=1.0, shift=0.0, first=None, norm=None, x_copy=None):
+    """One input segment of dense_rows: x [rows, ld] (or, with `first` = a K=1 nn.Linear, one value
+    per row at x[r * ld]); `norm` = an nn.LayerNorm applied with LeakyReLU(0.01) after it."""
+    inp = _lib.DenseInput()
+    inp.x = x.data_ptr()
+    inp.scale, inp.shift = float(scale), float(shift)
+    if first is not None:
+        inp.w1, inp.b1 = first.weight.data_ptr(), first.bias.data_ptr()
+        inp.width = first.out_features
+    else:
+        inp.width = int(width if width is not None else x.shape[-1])
+    inp.ld = int(ld if ld is not None else inp.width)
+    if norm is not None:
+        if norm.eps != 1e-5 or norm.weight is None:
+            raise RuntimeError("dense_input: LayerNorm(eps=1e-5, elementwise_affine) expected")
+        inp.gamma, inp.beta = norm.weight.data_ptr(), norm.bias.data_ptr()
+    if x_copy is not None:
+        inp.x_copy = x_copy.data_ptr()
+    return inp
+
+
+def dense_rows(problems, rows, device):
+    """ddsp_hip_dense_rows: up to two Linears (each `(inputs, linear, y)`, inputs from dense_input,
+    y [rows, out_features] contiguous) over `rows` <= 8 rows in one launch (core.py:122-129 blocks
+    with the LayerNorm/LeakyReLU of the previous block folded into the input)."""
+    arr = (_lib.DenseProblem * len(problems))()
+    for i, (inputs, lin, y) in enumerate(problems):
+        P = arr[i]
+        for j, inp in enumerate(inputs):
+            P.inputs[j] = inp
+        P.n_inputs = len(inputs)
+        if sum(inp.width for inp in inputs) != lin.in_features:
+            raise RuntimeError("dense_rows: inputs do not add up to the Linear's in_features")
+        P.weight = lin.weight.data_ptr()
+        P.bias = lin.bias.data_ptr() if lin.bias is not None else None
+        P.y = y.data_ptr()
+        P.ldy = y.shape[-1]
+        P.out_features = lin.out_features
+    _lib.call("dense_rows", arr, len(problems), int(rows),
+              ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream))
 
 
 # ------------------------------------------------------------------------------------

@@ -1,0 +1,205 @@
+// The decoder's control network for a few frames at a time (the realtime stream: 4 frames per
+// 1024-sample call, BASELINE.json config 3).  ddsp/core.py:122-129 builds every MLP block as
+// Linear -> LayerNorm -> LeakyReLU; decoder.py:43-68 chains three such MLPs, the GRU input
+// projection, the output MLP and the two projections (decoder.py:107-114).  At 4 rows each of
+// those ~25 torch ops is a launch-bound kernel of ~4-6 us (rocprofv3, 190 us per call).
+//
+// Here one launch computes one Linear for every row, with the previous block's LayerNorm +
+// LeakyReLU (and a K=1 first Linear, the loudness normalisation, the concatenations of
+// decoder.py:49,68) folded into how it reads its inputs:
+//   a[r, :] = concat_s act_s(x_s[r, :])                     (built in LDS, rows x K)
+//   y[r, n] = sum_k W[n, k] a[r, k] + b[n]                   (one wave per output row of W)
+// act_s: x' = x * scale + shift; if w1: x'' = w1[c] * x' + b1[c] (c < width; x' is one value per
+// row); if gamma: leaky_relu(layer_norm(x'') * gamma + beta, 0.01) with torch's eps 1e-5 and
+// biased variance.  W rows are streamed once per launch with coalesced loads; each workgroup
+// recomputes the (tiny) activations.  Up to kMaxProblems independent Linears share a launch
+// (blockIdx.y), e.g. the f0 and loudness MLPs, or the harmonic and noise projections.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace ddsp {
+namespace {
+
+constexpr int kDenseNT = 256;      // 4 waves
+constexpr int kOutPerWave = 2;     // output features per wave
+constexpr int kOutPerWG = (kDenseNT / 64) * kOutPerWave;
+constexpr int kMaxRows = 8;
+constexpr int kKL = 17;            // K <= 64 * kKL per lane-strided row (1088: the GRU input's 1024)
+
+struct DenseArgs {
+  ddsp_hip_dense_problem p[DDSP_HIP_DENSE_MAX_PROBLEMS];
+  int rows;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// At 4 rows everything here is latency: every global load a wave needs is issued before the
+// first use (W rows straight into registers at kernel entry, under the activation prologue),
+// and the cross-lane sums run step-major so their shuffles overlap.
+__global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
+  extern __shared__ float act[];  // [rows][K]
+  const ddsp_hip_dense_problem& P = args.p[blockIdx.y];
+  const int n0 = blockIdx.x * kOutPerWG;
+  if (n0 >= P.out_features) return;
+  const int rows = args.rows, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int K = 0;
+  for (int s = 0; s < P.n_inputs; ++s) K += (int)P.inputs[s].width;
+
+  // ---- W rows of this wave's outputs into registers ----
+  float wreg[kOutPerWave][kKL];
+#pragma unroll
+  for (int i = 0; i < kOutPerWave; ++i) {
+    const int n = min(n0 + wave * kOutPerWave + i, (int)P.out_features - 1);
+    const float* wr = P.weight + (int64_t)n * K;
+#pragma unroll
+    for (int j = 0; j < kKL; ++j) {
+      const int k = lane + 64 * j;
+      wreg[i][j] = k < K ? wr[k] : 0.0f;
+    }
+  }
+
+  // ---- activations: wave w builds (segment, row) pairs w, w+4, ... ----
+  int col0 = 0;
+  for (int s = 0; s < P.n_inputs; ++s) {
+    const ddsp_hip_dense_input& in = P.inputs[s];
+    const int width = (int)in.width;
+    for (int r = wave; r < rows; r += kDenseNT / 64) {
+      const float* xr = in.x + (int64_t)r * in.ld;
+      float* ar = act + (int64_t)r * K + col0;
+      float v[kKL], gm[kKL], bt[kKL];
+      if (in.gamma) {  // issued with the inputs, before the first reduction
+#pragma unroll
+        for (int j = 0; j < kKL; ++j) {
+          const int c = lane + 64 * j;
+          gm[j] = c < width ? in.gamma[c] : 0.0f;
+          bt[j] = c < width ? in.beta[c] : 0.0f;
+        }
+      }
+      float sum = 0.0f;
+      if (in.w1) {
+        const float xs = fmaf(xr[0], in.scale, in.shift);
+        if (in.x_copy && blockIdx.x == 0 && lane == 0) in.x_copy[r] = xs;
+#pragma unroll
+        for (int j = 0; j < kKL; ++j) {
+          const int c = lane + 64 * j;
+          v[j] = c < width ? fmaf(in.w1[c], xs, in.b1[c]) : 0.0f;
+          sum += v[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kKL; ++j) {
+          const int c = lane + 64 * j;
+          v[j] = c < width ? fmaf(xr[c], in.scale, in.shift) : 0.0f;
+          sum += v[j];
+        }
+      }
+      if (in.gamma) {  // LayerNorm (two-pass, biased variance) + LeakyReLU over this segment
+        const float mean = wave_sum(sum) / (float)width;
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kKL; ++j) {
+          const float d = lane + 64 * j < width ? v[j] - mean : 0.0f;
+          sq += d * d;
+        }
+        const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)width + 1e-5f);
+#pragma unroll
+        for (int j = 0; j < kKL; ++j) {
+          const float t = (v[j] - mean) * rstd * gm[j] + bt[j];
+          v[j] = t >= 0.0f ? t : 0.01f * t;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kKL; ++j)
+        if (lane + 64 * j < width) ar[lane + 64 * j] = v[j];
+    }
+    col0 += width;
+  }
+  __syncthreads();
+
+  // ---- GEMV from registers x LDS, then step-major wave sums ----
+  float acc[kOutPerWave][kMaxRows];
+#pragma unroll
+  for (int i = 0; i < kOutPerWave; ++i)
+#pragma unroll
+    for (int r = 0; r < kMaxRows; ++r) acc[i][r] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kKL; ++j) {
+    const int k = lane + 64 * j;
+    if (k < K) {
+#pragma unroll
+      for (int r = 0; r < kMaxRows; ++r) {
+        if (r < rows) {
+          const float a = act[r * K + k];
+#pragma unroll
+          for (int i = 0; i < kOutPerWave; ++i) acc[i][r] = fmaf(wreg[i][j], a, acc[i][r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < kOutPerWave; ++i)
+#pragma unroll
+      for (int r = 0; r < kMaxRows; ++r)
+        if (r < rows) acc[i][r] += __shfl_xor(acc[i][r], o, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < kOutPerWave; ++i) {
+      const int n = n0 + wave * kOutPerWave + i;
+      if (n < P.out_features) {
+        const float bn = P.bias ? P.bias[n] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < kMaxRows; ++r)
+          if (r < rows) P.y[(int64_t)r * P.ldy + n] = acc[i][r] + bn;
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace ddsp
+
+using namespace ddsp;
+
+extern "C" {
+
+int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream) {
+  if (!problems || n_problems < 1 || n_problems > DDSP_HIP_DENSE_MAX_PROBLEMS || rows < 0) return DDSP_HIP_EINVAL;
+  if (rows == 0) return DDSP_HIP_OK;
+  if (rows > kMaxRows) return DDSP_HIP_ERANGE;
+  DenseArgs args{};
+  args.rows = (int)rows;
+  int64_t max_n = 0, max_k = 0;
+  for (int i = 0; i < n_problems; ++i) {
+    const ddsp_hip_dense_problem& P = problems[i];
+    if (!P.weight || !P.y || P.out_features < 1 || P.n_inputs < 1 || P.n_inputs > DDSP_HIP_DENSE_MAX_INPUTS ||
+        P.ldy < P.out_features)
+      return DDSP_HIP_EINVAL;
+    int64_t K = 0;
+    for (int s = 0; s < P.n_inputs; ++s) {
+      const ddsp_hip_dense_input& in = P.inputs[s];
+      if (!in.x || in.width < 1 || (in.gamma && !in.beta) || (in.w1 && !in.b1)) return DDSP_HIP_EINVAL;
+      if (!in.w1 && in.ld < in.width) return DDSP_HIP_EINVAL;
+      if (in.width > 64 * kKL) return DDSP_HIP_ERANGE;
+      K += in.width;
+    }
+    max_n = std::max<int64_t>(max_n, P.out_features);
+    max_k = std::max(max_k, K);
+    args.p[i] = P;
+  }
+  const size_t shm = sizeof(float) * (size_t)rows * (size_t)max_k;
+  if (max_k > 64 * kKL || max_n > (int64_t)65535 * kOutPerWG) return DDSP_HIP_ERANGE;
+  const dim3 grid((unsigned)((max_n + kOutPerWG - 1) / kOutPerWG), (unsigned)n_problems);
+  hipLaunchKernelGGL(dense_rows_kernel, grid, dim3(kDenseNT), shm, reinterpret_cast<hipStream_t>(stream), args);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -31,7 +31,7 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
                                                        const float* __restrict__ b_hh, const float* __restrict__ h_prev,
                                                        int64_t hp_ld, float* __restrict__ h_out, int64_t ho_ld,
                                                        int B, int H, int64_t xp_ld, float* __restrict__ save,
-                                                       int64_t save_plane) {
+                                                       int64_t save_plane, float* __restrict__ h_copy) {
   extern __shared__ float smem[];
   constexpr int R = 3 * kHS;
   float* W = smem;                    // [R][H]
@@ -104,7 +104,9 @@ __global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__
     const float r = sigmoidf_(ex_r + (hr + eb_r));
     const float z = sigmoidf_(ex_z + (hz + eb_z));
     const float n = tanhf(ex_n + r * (hn + eb_n));
-    h_out[(int64_t)ebi * ho_ld + ej] = (1.0f - z) * n + z * ehp;
+    const float hn_t = (1.0f - z) * n + z * ehp;
+    h_out[(int64_t)ebi * ho_ld + ej] = hn_t;
+    if (h_copy) h_copy[(int64_t)ebi * H + ej] = hn_t;  // the last step's h_T, [B, H]
     if (save) {  // training: r, z, n and W_hn h + b_hn of this step, [4][B, T, H] (same row layout as h_out)
       float* sv = save + (int64_t)ebi * ho_ld + ej;
       sv[0] = r;
@@ -293,16 +295,19 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   const size_t shm = sizeof(float) * ((size_t)3 * kHS * H + (size_t)kKC * 3 * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
   const int64_t row = steps * hidden;  // out[b] row stride: [B, T, H]
+  // h_T goes to h_last from the last step's kernel, unless that step still reads h0 = h_last
+  const bool direct = h_last && steps > 1;
   for (int64_t t = 0; t < steps; ++t) {
     const float* hp = t == 0 ? h0 : out + (t - 1) * hidden;
     const int64_t hp_ld = t == 0 ? hidden : row;
     hipLaunchKernelGGL(gru_step_kernel, grid, dim3(kNT), shm, reinterpret_cast<hipStream_t>(stream),
                        xp + t * 3 * hidden, w_hh, b_hh, hp, hp_ld, out + t * hidden, row, B, H, steps * 3 * hidden,
-                       gates ? gates + t * hidden : nullptr, batch * steps * hidden);
+                       gates ? gates + t * hidden : nullptr, batch * steps * hidden,
+                       direct && t == steps - 1 ? h_last : nullptr);
     int st = launch_status();
     if (st) return st;
   }
-  if (h_last) {
+  if (h_last && !direct) {
     hipError_t e = hipMemcpy2DAsync(h_last, sizeof(float) * hidden, out + (steps - 1) * hidden, sizeof(float) * row,
                                     sizeof(float) * hidden, batch, hipMemcpyDeviceToDevice,
                                     reinterpret_cast<hipStream_t>(stream));

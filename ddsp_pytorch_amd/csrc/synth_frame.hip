@@ -21,7 +21,10 @@ namespace {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-template <bool RNG>
+// SPLIT (few-frame launches, e.g. the realtime stream's 4 frames per call): the workgroup has
+// G times the threads of one 4-samples-per-thread frame and the oscillator bank runs one sample
+// per thread, so one frame's latency is spread over G times the waves.
+template <bool RNG, bool SPLIT>
 __global__ void __launch_bounds__(256) synth_frame_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
@@ -125,37 +128,71 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   const int j0 = 4 * tid;
   const bool active = j0 < bs;
   const double dinc = (double)phase_inc(pitch0, sr);
-  float w[4], acc[4];
-  bool fast = true;
+  float acc[4];
+  if (!SPLIT) {
+    float w[4];
+    bool fast = true;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    w[s] = (float)(S + (double)(j0 + s + 1) * dinc);  // omega = fl32(exact prefix)
-    acc[s] = 0.0f;
-    fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
-  }
-  if (active) {
-    if (fast) {
+    for (int s = 0; s < 4; ++s) {
+      w[s] = (float)(S + (double)(j0 + s + 1) * dinc);  // omega = fl32(exact prefix)
+      acc[s] = 0.0f;
+      fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
+    }
+    if (active) {
+      if (fast) {
 #pragma unroll 2
-      for (int k = 0; k < H4; ++k) {
-        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+        for (int k = 0; k < H4; ++k) {
+          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
-      }
-    } else {
-      for (int k = 0; k < H; ++k) {
-        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+          for (int s = 0; s < 4; ++s)
+            acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
+        }
+      } else {
+        for (int k = 0; k < H; ++k) {
+          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float xx = w[s] * c1.y;
-          acc[s] = fabsf(xx) < kFastArgLimit
-                       ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
-                       : fmaf(sin_slow(xx), c1.z, acc[s]);
+          for (int s = 0; s < 4; ++s) {
+            const float xx = w[s] * c1.y;
+            acc[s] = fabsf(xx) < kFastArgLimit
+                         ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
+                         : fmaf(sin_slow(xx), c1.z, acc[s]);
+          }
         }
       }
     }
+    __syncthreads();  // tail[] complete
+  } else {
+    // SPLIT: every thread takes samples j = tid, tid + NT, ... (the same per-sample sum over k in
+    // the same order as above, so the result does not depend on the launch shape); the samples
+    // meet their quad's thread through LDS after x[]
+    float* hsum = x + bs;
+    for (int j = tid; j < bs; j += NT) {
+      const float wj = (float)(S + (double)(j + 1) * dinc);
+      float a = 0.0f;
+      if (fabsf(wj) * (float)H4 < kFastArgLimit) {
+        for (int k = 0; k < H4; ++k) {
+          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+          a = amp_sin_acc(reduce_signed(wj * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, a);
+        }
+      } else {
+        for (int k = 0; k < H; ++k) {
+          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+          const float xx = wj * c1.y;
+          a = fabsf(xx) < kFastArgLimit ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, a)
+                                        : fmaf(sin_slow(xx), c1.z, a);
+        }
+      }
+      hsum[j] = a;
+    }
+    __syncthreads();  // tail[] and hsum[] complete
+    if (active) {
+      const float4 h4 = *reinterpret_cast<const float4*>(hsum + j0);
+      acc[0] = h4.x;
+      acc[1] = h4.y;
+      acc[2] = h4.z;
+      acc[3] = h4.w;
+    }
   }
-  __syncthreads();  // tail[] complete
   if (!active) return;
 
   // ---- phase 6: filtered noise for the same samples, sum, store ----
@@ -209,20 +246,28 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   const int H4 = ((int)n_harmonic + 3) & ~3, n4 = (n + 3) & ~3;
   const size_t floats = (size_t)8 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs +
                         ((half + 3) & ~3) + pad + bs;
-  const size_t shm = sizeof(float) * floats;
-  if (shm > 120 * 1024) return DDSP_HIP_ERANGE;
+  if (sizeof(float) * floats > 120 * 1024) return DDSP_HIP_ERANGE;
   const int nt = std::max(64, ((bs / 4 + 63) / 64) * 64);
+  // few frames (far fewer workgroups than CUs): split each frame's harmonics over G thread groups
+  int G = batch * frames < 512 ? std::max(1, std::min(4, 256 / nt)) : 1;
+  if (sizeof(float) * (floats + (size_t)bs) > 120 * 1024) G = 1;
+  const size_t shm = sizeof(float) * (floats + (G > 1 ? (size_t)bs : 0));
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
-  const dim3 grid((unsigned)frames, (unsigned)batch);
-  if (noise)
-    hipLaunchKernelGGL(synth_frame_kernel<false>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
-                       bias, noise, k0, k1, o0, o1, nullptr, out, harmonic_out, noise_out, (int)frames,
-                       (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
-  else
-    hipLaunchKernelGGL(synth_frame_kernel<true>, grid, dim3(nt), shm, S(stream), f0, param, raw_magnitudes,
-                       bias, nullptr, k0, k1, o0, o1, counter, out, harmonic_out, noise_out, (int)frames,
-                       (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad);
+  const dim3 grid((unsigned)frames, (unsigned)batch), block((unsigned)(nt * G));
+#define DDSP_SYNTH_FRAME_LAUNCH(RNG_, SPLIT_)                                                              \
+  hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
+                     bias, RNG_ ? nullptr : noise, k0, k1, o0, o1, RNG_ ? counter : nullptr, out, harmonic_out,  \
+                     noise_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, \
+                     pad)
+  if (noise) {
+    if (G > 1) DDSP_SYNTH_FRAME_LAUNCH(false, true);
+    else DDSP_SYNTH_FRAME_LAUNCH(false, false);
+  } else {
+    if (G > 1) DDSP_SYNTH_FRAME_LAUNCH(true, true);
+    else DDSP_SYNTH_FRAME_LAUNCH(true, false);
+  }
+#undef DDSP_SYNTH_FRAME_LAUNCH
   if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
   return launch_status();
 }

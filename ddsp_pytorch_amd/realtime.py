@@ -10,14 +10,22 @@ synthesis), so its latency is launch-bound, not compute-bound.
 `RealtimeGraph` captures one call — loudness normalisation, decimation by block_size, the
 control network with the cached GRU state, the fused synthesis kernel — into a HIP graph
 (`torch.cuda.CUDAGraph` is hipGraph on ROCm) over static device buffers, and replays it per
-call: one graph launch plus the two host<->device copies.  The on-device noise takes its
+call: one graph launch plus the two host<->device copies.  With `fused=True` (default) the
+control network runs on `ddsp_hip_dense_rows` (csrc/dense.hip): each Linear one launch with the
+previous block's LayerNorm + LeakyReLU, the first K=1 Linear, the loudness normalisation and
+the concatenations folded into its input — 7 launches + the GRU steps + the synthesis instead
+of ~30 torch kernels.  The on-device noise takes its
 Philox offset from a device counter the graph advances (`ddsp_hip_synth_frames_counter`), so
 every replay draws fresh noise; call k equals the eager model run with noise offset k.
 """
+from collections import namedtuple
+
 import torch
 
 from . import core
 from .decoder import gru_decoder_forward
+
+_Linear = namedtuple("_Linear", "weight bias in_features out_features")
 
 
 class RealtimeGraph:
@@ -30,7 +38,7 @@ class RealtimeGraph:
     with memcpy)."""
 
     def __init__(self, model, call_samples=1024, mean_loudness=0.0, std_loudness=1.0,
-                 seed=0x5EEDDD5B, device=None, warmup=3):
+                 seed=0x5EEDDD5B, device=None, warmup=3, fused=True):
         device = torch.device(device) if device is not None else next(model.parameters()).device
         if device.type != "cuda":
             raise RuntimeError("RealtimeGraph: the model must be on a HIP device")
@@ -56,6 +64,9 @@ class RealtimeGraph:
         self._pitch_h = torch.zeros(1, N, 1).pin_memory()
         self._loud_h = torch.zeros(1, N, 1).pin_memory()
         self._out_h = torch.zeros(1, N, 1).pin_memory()
+        self.fused = bool(fused)
+        if self.fused:
+            self._setup_fused()
         self.graph = torch.cuda.CUDAGraph()
         cache0 = model.decoder.cache_gru.detach().clone()
         side = torch.cuda.Stream(device)
@@ -70,8 +81,60 @@ class RealtimeGraph:
         model.decoder.cache_gru.copy_(cache0)
         self.counter.zero_()
 
+    def _setup_fused(self):
+        m, dev = self.model, self.device
+        d = m.decoder
+        if not core.gru_supported(d.gru):
+            raise RuntimeError("RealtimeGraph(fused=True): GRU shape outside the step kernel's")
+        for seq in (d.f0_mlp, d.loudness_mlp, d.out_mlp):
+            if len(seq) != 9 or any(seq[i].negative_slope != 0.01 for i in (2, 5, 8)):
+                raise RuntimeError("RealtimeGraph(fused=True): mlp(.., .., 3) blocks of core.py:122-129 expected")
+        R = self.call_samples // self.block_size
+        if R > 8:
+            raise RuntimeError("RealtimeGraph(fused=True): at most 8 frames per call")
+        Hd = d.gru.hidden_size
+        z = lambda n: torch.zeros(R, n, device=dev)
+        self._buf = {"y2f": z(Hd), "y2l": z(Hd), "y3f": z(Hd), "y3l": z(Hd), "xp": z(3 * Hd),
+                     "gru": z(Hd), "y4": z(Hd), "y5": z(Hd), "y6": z(Hd),
+                     "param": z(m.harmonic_proj.out_features), "mags": z(m.noise_proj.out_features),
+                     "f0": z(1), "loud": z(1)}
+
+    def _forward_fused(self):
+        """The same forward on ddsp_hip_dense_rows: decoder.py:43-68 + the projections
+        (decoder.py:107-114) in 7 launches, the GRU on its step kernel, then the synthesis."""
+        m, d, bs, b = self.model, self.model.decoder, self.block_size, self._buf
+        R, dev = self.call_samples // bs, self.device
+        di = core.dense_input
+        inv = 1.0 / self.std_loudness
+        f0m, lm, om = d.f0_mlp, d.loudness_mlp, d.out_mlp
+        core.dense_rows([  # mlp layers 1-2 (core.py:122-129), f0 and loudness
+            ([di(self.pitch, ld=bs, first=f0m[0], norm=f0m[1], x_copy=b["f0"])], f0m[3], b["y2f"]),
+            ([di(self.loudness, ld=bs, scale=inv, shift=-self.mean_loudness * inv, first=lm[0], norm=lm[1],
+                 x_copy=b["loud"])], lm[3], b["y2l"])], R, dev)
+        core.dense_rows([([di(b["y2f"], norm=f0m[4])], f0m[6], b["y3f"]),
+                         ([di(b["y2l"], norm=lm[4])], lm[6], b["y3l"])], R, dev)
+        # GRU input projection of cat([f0_mlp(f0), loudness_mlp(loudness)]) (decoder.py:49)
+        g = d.gru
+        w_ih = _Linear(g.weight_ih_l0, g.bias_ih_l0, g.input_size, 3 * g.hidden_size)
+        core.dense_rows([([di(b["y3f"], norm=f0m[7]), di(b["y3l"], norm=lm[7])], w_ih, b["xp"])], R, dev)
+        cache = d.cache_gru
+        core._lib.call("gru_forward", core._lib.ptr(b["xp"]), core._lib.ptr(g.weight_hh_l0), core._lib.ptr(g.bias_hh_l0),
+                       core._lib.ptr(cache), core._lib.ptr(b["gru"]), core._lib.ptr(cache), None, 1, R,
+                       g.hidden_size, core._lib.stream_of(cache))
+        # out_mlp(cat([gru_out, f0, loudness])) (decoder.py:68), then the projections
+        core.dense_rows([([di(b["gru"]), di(b["f0"]), di(b["loud"])], om[0], b["y4"])], R, dev)
+        core.dense_rows([([di(b["y4"], norm=om[1])], om[3], b["y5"])], R, dev)
+        core.dense_rows([([di(b["y5"], norm=om[4])], om[6], b["y6"])], R, dev)
+        core.dense_rows([([di(b["y6"], norm=om[7])], m.harmonic_proj, b["param"]),
+                         ([di(b["y6"], norm=om[7])], m.noise_proj, b["mags"])], R, dev)
+        return core.synth_frames_counter(b["f0"].view(1, R, 1), b["param"].view(1, R, -1),
+                                         b["mags"].view(1, R, -1), bs, self.sample_rate, self.counter,
+                                         self.seed, bias=self.bias)
+
     def _forward(self):
         """export.py:33-40 realtime ScriptDDSP.forward with the model's synthesis fused."""
+        if self.fused:
+            return self._forward_fused()
         m, bs = self.model, self.block_size
         pitch = self.pitch[:, ::bs]
         loudness = (self.loudness[:, ::bs] - self.mean_loudness) / self.std_loudness

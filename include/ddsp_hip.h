@@ -170,6 +170,41 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* ---------------- the decoder network for a few frames: core.py:122-129, decoder.py:43-68 ----------------
+ * One Linear for rows <= 8 frames (the realtime stream's 1024-sample calls, ddsp_model.cpp:32-52)
+ * with the previous MLP block's LayerNorm + LeakyReLU folded into its input:
+ *   a[r, :] = concat over inputs s of act_s(x_s[r, :])
+ *   y[r, n] = sum_k weight[n, k] a[r, k] + bias[n]          weight [out_features, K] (nn.Linear)
+ * act_s: x' = x * scale + shift (the exported model's loudness normalisation, export.py:35;
+ * 1 and 0 otherwise); with w1/b1 (a K=1 nn.Linear of width `width`, the first layer of
+ * core.py:122's mlp(1, ...)) x is one value per row and x'' = w1[c] * x' + b1[c]; with
+ * gamma/beta: leaky_relu(layer_norm(x'') * gamma + beta, 0.01), eps 1e-5 (core.py:126).
+ * x_copy (nullable, w1 inputs only) receives x' per row.  Up to DDSP_HIP_DENSE_MAX_PROBLEMS
+ * independent Linears share one launch.  rows <= 8, K <= 1088 (else DDSP_HIP_ERANGE). */
+#define DDSP_HIP_DENSE_MAX_INPUTS 3
+#define DDSP_HIP_DENSE_MAX_PROBLEMS 2
+typedef struct ddsp_hip_dense_input {
+  const float* x;      /* [rows, ld] (w1 inputs: x[r * ld] is the row's value) */
+  int64_t ld;
+  int64_t width;       /* columns contributed to K */
+  float scale, shift;
+  const float* w1;     /* nullable [width] */
+  const float* b1;     /* [width] when w1 */
+  const float* gamma;  /* nullable [width]: LayerNorm + LeakyReLU */
+  const float* beta;
+  float* x_copy;       /* nullable [rows] */
+} ddsp_hip_dense_input;
+typedef struct ddsp_hip_dense_problem {
+  ddsp_hip_dense_input inputs[DDSP_HIP_DENSE_MAX_INPUTS];
+  int n_inputs;
+  const float* weight; /* [out_features, K] */
+  const float* bias;   /* nullable [out_features] */
+  float* y;            /* [rows, ldy] */
+  int64_t ldy;
+  int64_t out_features;
+} ddsp_hip_dense_problem;
+int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream);
+
 /* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
  * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,
  * computed by the caller's GEMM), W_hh[3H,H], b_hh[3H] in torch's (r, z, n) order; h0 [B,H]

@@ -12,7 +12,7 @@ gpu = pytest.mark.gpu
 BS, H, NB, N = 256, 64, 65, 1024
 
 
-def _model(hidden=64, seed=0):
+def _model(hidden=512, seed=0):
     import ddsp_pytorch_amd as dd
     torch.manual_seed(seed)
     m = dd.DDSPDecoder(hidden, H, NB, 48000, BS, False).eval()
@@ -52,21 +52,29 @@ def test_realtime_graph_needs_device():
 
 
 @gpu
-def test_realtime_graph_matches_eager_calls():
+@pytest.mark.parametrize("fused", [False, True])
+def test_realtime_graph_matches_eager_calls(fused):
+    """fused=False replays the eager kernels (bit-equal); fused=True runs the control network on
+    ddsp_hip_dense_rows (different fp32 summation order: ≤1e-5 RMS on the audio)."""
     from ddsp_pytorch_amd.realtime import RealtimeGraph
     from oracle import torch_ref as tr
     dev = torch.device("cuda", 0)
     mean, std, seed = -3.0, 1.5, 77
     mg = _model().to(dev)
     me = _model().to(dev)
-    rt = RealtimeGraph(mg, N, mean, std, seed=seed)
+    rt = RealtimeGraph(mg, N, mean, std, seed=seed, fused=fused)
     with torch.no_grad():
         for k, (pitch, loud) in enumerate(_calls(5)):
             y = rt(pitch, loud).clone()
             ye, he, param, p = _eager(me, pitch.to(dev), loud.to(dev), k, seed, mean, std)
             assert y.shape == (1, N, 1) and not y.is_cuda
-            assert float((y - ye.cpu()).abs().max()) <= 1e-6, k
-            assert torch.allclose(mg.decoder.cache_gru, me.decoder.cache_gru, atol=1e-6)
+            if fused:
+                assert rms(y.numpy(), ye.cpu().numpy()) <= 1e-5, k
+                assert float((y - ye.cpu()).abs().max()) <= 1e-4, k
+                assert torch.allclose(mg.decoder.cache_gru, me.decoder.cache_gru, atol=1e-5)
+            else:
+                assert float((y - ye.cpu()).abs().max()) <= 1e-6, k
+                assert torch.allclose(mg.decoder.cache_gru, me.decoder.cache_gru, atol=1e-6)
             # harmonic part against the oracle (modules.py:44-80 on the CPU)
             pc = param.cpu()
             amp, dist = tr.harmonic_controls(pc[..., :1], pc[..., 1:], p.cpu(), 48000)
@@ -108,3 +116,40 @@ def test_realtime_graph_rejects_bad_shapes():
     rt = RealtimeGraph(_model().to(dev), N)
     with pytest.raises(RuntimeError):
         rt(torch.zeros(1, 512, 1), torch.zeros(1, 512, 1))
+
+
+@gpu
+def test_dense_rows_matches_torch_blocks():
+    """ddsp_hip_dense_rows against torch: Linear of [LeakyReLU(LayerNorm(x))] for a K=1 first
+    layer with input normalisation, a plain block, and a three-way concatenation of raw inputs."""
+    import torch.nn as nn
+    from ddsp_pytorch_amd import core
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    R = 5
+    l1, ln1, l2 = nn.Linear(1, 96).to(dev), nn.LayerNorm(96).to(dev), nn.Linear(96, 80).to(dev)
+    with torch.no_grad():
+        ln1.weight.normal_(1, 0.2)
+        ln1.bias.normal_(0, 0.2)
+    x = torch.randn(R, 7, device=dev)  # column 0 per row, ld 7
+    y = torch.empty(R, 80, device=dev)
+    xc = torch.empty(R, 1, device=dev)
+    core.dense_rows([([core.dense_input(x, ld=7, scale=0.5, shift=1.0, first=l1, norm=ln1, x_copy=xc)], l2, y)],
+                    R, dev)
+    with torch.no_grad():
+        xs = x[:, :1] * 0.5 + 1.0
+        ref = l2(nn.functional.leaky_relu(ln1(l1(xs)), 0.01))
+    torch.cuda.synchronize()
+    assert torch.allclose(xc, xs)
+    assert torch.allclose(y, ref, atol=2e-5, rtol=1e-5)
+    # concatenation of raw segments (decoder.py:68)
+    a, b, c = torch.randn(R, 64, device=dev), torch.randn(R, 1, device=dev), torch.randn(R, 1, device=dev)
+    l3 = nn.Linear(66, 33).to(dev)
+    y3 = torch.empty(R, 33, device=dev)
+    core.dense_rows([([core.dense_input(a), core.dense_input(b), core.dense_input(c)], l3, y3)], R, dev)
+    with torch.no_grad():
+        ref3 = l3(torch.cat([a, b, c], -1))
+    assert torch.allclose(y3, ref3, atol=2e-5, rtol=1e-5)
+    with pytest.raises(RuntimeError):  # more than 8 rows
+        core.dense_rows([([core.dense_input(torch.randn(9, 66, device=dev))], l3, torch.empty(9, 33, device=dev))],
+                        9, dev)

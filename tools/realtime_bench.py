@@ -42,33 +42,36 @@ def main():
     lat = sorted(lat[20:])
     res = {"python_loop": {"mean_ms": statistics.mean(lat), "p50_ms": lat[len(lat) // 2],
                            "p99_ms": lat[int(0.99 * len(lat))], "budget_ms": 1024 / 48.0}}
-    # the same model on a captured HIP graph (ddsp_pytorch_amd.realtime), device noise
+    # the same model on a captured HIP graph (ddsp_pytorch_amd.realtime), device noise; the
+    # control network either on csrc/dense.hip (fused) or as torch's kernels inside the graph
     from ddsp_pytorch_amd.realtime import RealtimeGraph
-    rt = RealtimeGraph(m, 1024)
-    lat = []
-    with torch.no_grad():
-        for i in range(args.calls):
-            p = torch.full((1, 1024, 1), 220.0 * 2 ** ((i // 20) % 12 / 12))
-            t0 = time.perf_counter()
-            y = rt(p, loud.cpu())
-            lat.append((time.perf_counter() - t0) * 1e3)
-    assert torch.isfinite(y).all()
-    pd, ld = p.cuda(), loud
-    for _ in range(20):
-        rt(pd, ld)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(200):
-        rt(pd, ld)
-    e1.record()
-    torch.cuda.synchronize()
-    gpu_ms = e0.elapsed_time(e1) / 200
-    lat = sorted(lat[20:])
-    res["hip_graph"] = {"mean_ms": statistics.mean(lat), "p50_ms": lat[len(lat) // 2],
-                        "p99_ms": lat[int(0.99 * len(lat))], "budget_ms": 1024 / 48.0,
-                        "device_ms_per_replay": gpu_ms,
-                        "what": "host pitch/loudness -> one hipGraph replay (control network + fused "
-                                "synthesis) -> host audio"}
+    for key, fused in (("hip_graph", True), ("hip_graph_torch_net", False)):
+        rt = RealtimeGraph(m, 1024, fused=fused)
+        lat = []
+        with torch.no_grad():
+            for i in range(args.calls):
+                p = torch.full((1, 1024, 1), 220.0 * 2 ** ((i // 20) % 12 / 12))
+                t0 = time.perf_counter()
+                y = rt(p, loud.cpu())
+                lat.append((time.perf_counter() - t0) * 1e3)
+            assert torch.isfinite(y).all()
+            pd, ld = p.cuda(), loud
+            for _ in range(20):
+                rt(pd, ld)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(200):
+                rt(pd, ld)
+            e1.record()
+            torch.cuda.synchronize()
+        gpu_ms = e0.elapsed_time(e1) / 200
+        lat = sorted(lat[20:])
+        res[key] = {"mean_ms": statistics.mean(lat), "p50_ms": lat[len(lat) // 2],
+                    "p99_ms": lat[int(0.99 * len(lat))], "budget_ms": 1024 / 48.0,
+                    "device_ms_per_replay": gpu_ms,
+                    "what": "host pitch/loudness -> one hipGraph replay (control network "
+                            + ("on csrc/dense.hip" if fused else "as torch kernels") + " + GRU step kernel + fused "
+                            "synthesis) -> host audio"}
     host = os.path.join(ROOT, "tools", "realtime_host")
     if os.path.exists(host):
         r = subprocess.run([host, path, os.path.join(ROOT, "ddsp_pytorch_amd", "lib", "libddsp_hip_torch.so"),
