@@ -23,8 +23,8 @@
 namespace ddsp {
 namespace {
 
-constexpr int kDenseNT = 256;      // 4 waves
-constexpr int kOutPerWave = 2;     // output features per wave
+constexpr int kDenseNT = 512;      // 8 waves
+constexpr int kOutPerWave = 1;     // output features per wave
 constexpr int kOutPerWG = (kDenseNT / 64) * kOutPerWave;
 constexpr int kMaxRows = 8;
 constexpr int kKL = 17;            // K <= 64 * kKL per lane-strided row (1088: the GRU input's 1024)
@@ -34,34 +34,46 @@ struct DenseArgs {
   int rows;
 };
 
+// Sum over the wave, returned uniform: DPP quad permutes for lane distances 1 and 2,
+// ds_swizzle xor for 4, 8, 16 (within each half), then the two halves by readlane — no
+// ds_bpermute address arithmetic, no LDS round trip (the 6-step __shfl_xor tree cost ~3 us of
+// a 10 us launch here).
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));  // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x101F));  // xor 4
+  v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x201F));  // xor 8
+  v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));  // xor 16
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
 }
 
 // At 4 rows everything here is latency: every global load a wave needs is issued before the
 // first use (W rows straight into registers at kernel entry, under the activation prologue),
-// and the cross-lane sums run step-major so their shuffles overlap.
+// and the cross-lane sums avoid ds_bpermute.
 __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
   extern __shared__ float act[];  // [rows][K]
   const ddsp_hip_dense_problem& P = args.p[blockIdx.y];
   const int n0 = blockIdx.x * kOutPerWG;
   if (n0 >= P.out_features) return;
-  const int rows = args.rows, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rows = args.rows, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar row bases
   int K = 0;
   for (int s = 0; s < P.n_inputs; ++s) K += (int)P.inputs[s].width;
 
   // ---- W rows of this wave's outputs into registers ----
   float wreg[kOutPerWave][kKL];
+  // (loads branch-free: a clamped address and a select; chunk guards j < nK are wave-uniform)
+  const int nK = (K + 63) >> 6;
 #pragma unroll
   for (int i = 0; i < kOutPerWave; ++i) {
     const int n = min(n0 + wave * kOutPerWave + i, (int)P.out_features - 1);
     const float* wr = P.weight + (int64_t)n * K;
 #pragma unroll
     for (int j = 0; j < kKL; ++j) {
-      const int k = lane + 64 * j;
-      wreg[i][j] = k < K ? wr[k] : 0.0f;
+      const unsigned k = lane + 64 * j;
+      const float w = wr[min(k, (unsigned)K - 1u)];  // unconditional: every address is valid
+      wreg[i][j] = k < (unsigned)K ? w : 0.0f;
     }
   }
 
@@ -73,13 +85,14 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
     for (int r = wave; r < rows; r += kDenseNT / 64) {
       const float* xr = in.x + (int64_t)r * in.ld;
       float* ar = act + (int64_t)r * K + col0;
+      const int nC = (width + 63) >> 6;
       float v[kKL], gm[kKL], bt[kKL];
       if (in.gamma) {  // issued with the inputs, before the first reduction
 #pragma unroll
         for (int j = 0; j < kKL; ++j) {
-          const int c = lane + 64 * j;
-          gm[j] = c < width ? in.gamma[c] : 0.0f;
-          bt[j] = c < width ? in.beta[c] : 0.0f;
+          const int cc = min(lane + 64 * j, width - 1);
+          gm[j] = in.gamma[cc];
+          bt[j] = in.beta[cc];
         }
       }
       float sum = 0.0f;
@@ -88,15 +101,17 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
         if (in.x_copy && blockIdx.x == 0 && lane == 0) in.x_copy[r] = xs;
 #pragma unroll
         for (int j = 0; j < kKL; ++j) {
-          const int c = lane + 64 * j;
-          v[j] = c < width ? fmaf(in.w1[c], xs, in.b1[c]) : 0.0f;
+          const int cc = min(lane + 64 * j, width - 1);
+          const float t = fmaf(in.w1[cc], xs, in.b1[cc]);
+          v[j] = lane + 64 * j < width ? t : 0.0f;
           sum += v[j];
         }
       } else {
 #pragma unroll
         for (int j = 0; j < kKL; ++j) {
-          const int c = lane + 64 * j;
-          v[j] = c < width ? fmaf(xr[c], in.scale, in.shift) : 0.0f;
+          const int cc = min(lane + 64 * j, width - 1);
+          const float t = fmaf(xr[cc], in.scale, in.shift);
+          v[j] = lane + 64 * j < width ? t : 0.0f;
           sum += v[j];
         }
       }
@@ -117,7 +132,7 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
       }
 #pragma unroll
       for (int j = 0; j < kKL; ++j)
-        if (lane + 64 * j < width) ar[lane + 64 * j] = v[j];
+        if (j < nC && lane + 64 * j < width) ar[lane + 64 * j] = v[j];
     }
     col0 += width;
   }
@@ -131,8 +146,8 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
     for (int r = 0; r < kMaxRows; ++r) acc[i][r] = 0.0f;
 #pragma unroll
   for (int j = 0; j < kKL; ++j) {
-    const int k = lane + 64 * j;
-    if (k < K) {
+    if (j < nK) {  // wave-uniform; past K the weights are 0 and the activation index is clamped
+      const int k = min(lane + 64 * j, K - 1);
 #pragma unroll
       for (int r = 0; r < kMaxRows; ++r) {
         if (r < rows) {
@@ -144,12 +159,10 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
+  for (int i = 0; i < kOutPerWave; ++i)
 #pragma unroll
-    for (int i = 0; i < kOutPerWave; ++i)
-#pragma unroll
-      for (int r = 0; r < kMaxRows; ++r)
-        if (r < rows) acc[i][r] += __shfl_xor(acc[i][r], o, 64);
+    for (int r = 0; r < kMaxRows; ++r)
+      if (r < rows) acc[i][r] = wave_sum(acc[i][r]);
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < kOutPerWave; ++i) {
