@@ -58,11 +58,11 @@ class RealtimeGraph:
         self.std_loudness = float(std_loudness)
         self.seed = int(seed)
         self.bias = float(model.noise_synth.initial_bias)
-        self.pitch = torch.zeros(1, N, 1, device=device)
-        self.loudness = torch.zeros(1, N, 1, device=device)
+        # pitch and loudness share one buffer: one host->device copy per call
+        self._inp = torch.zeros(2, N, 1, device=device)
+        self.pitch, self.loudness = self._inp[0:1], self._inp[1:2]
         self.counter = torch.zeros(1, dtype=torch.int64, device=device)
-        self._pitch_h = torch.zeros(1, N, 1).pin_memory()
-        self._loud_h = torch.zeros(1, N, 1).pin_memory()
+        self._inp_h = torch.zeros(2, N, 1).pin_memory()
         self._out_h = torch.zeros(1, N, 1).pin_memory()
         self.fused = bool(fused)
         if self.fused:
@@ -160,10 +160,9 @@ class RealtimeGraph:
             self.loudness.copy_(loudness)
             self.graph.replay()
             return self.out
-        self._pitch_h.copy_(pitch)
-        self._loud_h.copy_(loudness)
-        self.pitch.copy_(self._pitch_h, non_blocking=True)
-        self.loudness.copy_(self._loud_h, non_blocking=True)
+        self._inp_h[0:1].copy_(pitch)
+        self._inp_h[1:2].copy_(loudness)
+        self._inp.copy_(self._inp_h, non_blocking=True)
         self.graph.replay()
         self._out_h.copy_(self.out, non_blocking=True)
         stream.synchronize()
