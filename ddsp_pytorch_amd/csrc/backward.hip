@@ -40,17 +40,8 @@ __device__ __forceinline__ float scale_fn_grad(float x) {
   return 2.0f * kLn10F * p * one_minus;
 }
 
-// acc + g * sin(x) for |x| < kFastArgLimit: the reduction and polynomial of sin_reduced with
-// g applied to the reduced argument (13 VALU ops).
-__device__ __forceinline__ float gsin_acc(float x, float g, float acc) {
-  const float rs = reduce_signed(x);
-  const float r2 = rs * rs;
-  float q = fmaf(kS9, r2, kS7);
-  q = fmaf(q, r2, kS5);
-  q = fmaf(q, r2, kS3);
-  q = fmaf(q, r2, 1.0f);
-  return fmaf(rs * g, q, acc);
-}
+// acc + g * sin(x) for |x| < kFastArgLimit.
+__device__ __forceinline__ float gsin_acc(float x, float g, float acc) { return fmaf(g, sin_reduced(x), acc); }
 
 // ---------------------------------------------------------------------------------------
 // scale_function backward: dx = g * scale_fn'(x + bias)
@@ -141,8 +132,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
   constexpr bool PARAMS = HMODE == 2;
   // LDS layout (mirrored by frame_backward_lds_floats): xl and gl start 16-B aligned
   const int hfl = HARM ? 2 * bs + NS * H + H : 0;
-  // (omega_t, g_t) per sample.  (Folding g into per-sample polynomial coefficients, 12 instead of
-  // 13 VALU ops per sine, measured 8% slower: three LDS reads per sample and a larger footprint.)
+  // (omega_t, g_t) per sample
   float2* wg = reinterpret_cast<float2*>(smem);  // [bs]
   float* part = smem + 2 * bs;                   // [NS * H]
   float* uk = part + NS * H;                     // [H] u_k (PARAMS: v_k first)
@@ -244,34 +234,16 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
         for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
           const float2 p = wg[j], p1 = wg[j + 1];
           // the 8 chains written stage by stage so the scheduler keeps them interleaved (ILP 8)
-          float x[2 * kKPT], t8[2 * kKPT], r8[2 * kKPT], q8[2 * kKPT];
+          float y[2 * kKPT];
 #pragma unroll
           for (int c = 0; c < kKPT; ++c) {
-            x[c] = p.x * kf[c];
-            x[kKPT + c] = p1.x * kf[c];
-          }
-#pragma unroll
-          for (int i = 0; i < 2 * kKPT; ++i) t8[i] = fmaf(x[i], kInvPi, kMagic);
-#pragma unroll
-          for (int i = 0; i < 2 * kKPT; ++i) {
-            const float nn = t8[i] - kMagic;
-            r8[i] = fmaf(-nn, kPiB, fmaf(-nn, kPiA, x[i]));
-          }
-#pragma unroll
-          for (int i = 0; i < 2 * kKPT; ++i)
-            r8[i] = __uint_as_float(__float_as_uint(r8[i]) + (__float_as_uint(t8[i]) << 31));
-#pragma unroll
-          for (int i = 0; i < 2 * kKPT; ++i) {
-            const float r2 = r8[i] * r8[i];
-            float q = fmaf(kS9, r2, kS7);
-            q = fmaf(q, r2, kS5);
-            q = fmaf(q, r2, kS3);
-            q8[i] = fmaf(q, r2, 1.0f);
+            y[c] = reduce_rev(p.x * kf[c]);
+            y[kKPT + c] = reduce_rev(p1.x * kf[c]);
           }
 #pragma unroll
           for (int c = 0; c < kKPT; ++c) {
-            acc[c] = fmaf(r8[c] * p.y, q8[c], acc[c]);
-            acc2[c] = fmaf(r8[kKPT + c] * p1.y, q8[kKPT + c], acc2[c]);
+            acc[c] = fmaf(p.y, sin_rev(y[c]), acc[c]);
+            acc2[c] = fmaf(p1.y, sin_rev(y[kKPT + c]), acc2[c]);
           }
         }
         if (j < j1) {

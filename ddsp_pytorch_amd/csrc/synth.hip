@@ -101,9 +101,9 @@ template <int SPT, bool RAW>
 __global__ void __launch_bounds__(256) harmonic_frames_kernel(
     const float* __restrict__ f0, const float* __restrict__ amp, float* dist, int write_back,
     float* __restrict__ out, int F, int H, int bs, float sr) {
-  // per harmonic k: coef[2k] = (A, A*S3, A*S5, A*S7), coef[2k+1] = (A*S9, k+1, A, 0), A = dist*amp;
-  // H rounded up to 4 with zero amplitudes.  Read back as wave-uniform (broadcast) LDS loads.
-  extern __shared__ float4 coef[];
+  // per harmonic k: coef[k] = (k+1, A), A = dist*amp; H rounded up to 4 with zero amplitudes.
+  // Read back as wave-uniform (broadcast) LDS loads.
+  extern __shared__ float2 coef[];
   __shared__ double red[16];
 
   const int f = blockIdx.x;
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
     double part2 = 0.0;
     for (int k = tid; k < H; k += NT) {
       const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
-      coef[2 * k].x = v;
+      coef[k].y = v;
       part2 += (double)v;
     }
     norm = (float)block_sum_double(part2, red);  // dist.sum(-1)
@@ -140,14 +140,13 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
     float v = 0.0f;
     if (k < H) {
       if (RAW) {
-        v = (coef[2 * k].x / norm) * a;  // (dist / sum) * amp, the reference's rounding order
+        v = (coef[k].y / norm) * a;  // (dist / sum) * amp, the reference's rounding order
       } else {
         v = dist[row * H + k] * a;
         if (write_back) dist[row * H + k] = v;
       }
     }
-    coef[2 * k] = make_float4(v, v * kS3, v * kS5, v * kS7);
-    coef[2 * k + 1] = make_float4(v * kS9, (float)(k + 1), v, 0.0f);
+    coef[k] = make_float2((float)(k + 1), v);
   }
   __syncthreads();
 
@@ -166,22 +165,19 @@ __global__ void __launch_bounds__(256) harmonic_frames_kernel(
       fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
     }
     if (fast) {
-#pragma unroll 2
+#pragma unroll 4
       for (int k = 0; k < H4; ++k) {
-        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+        const float2 c = coef[k];
 #pragma unroll
-        for (int s = 0; s < SPT; ++s)
-          acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
+        for (int s = 0; s < SPT; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
       }
     } else {
       for (int k = 0; k < H; ++k) {
-        const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+        const float2 c = coef[k];
 #pragma unroll
         for (int s = 0; s < SPT; ++s) {
-          const float x = w[s] * c1.y;
-          acc[s] = fabsf(x) < kFastArgLimit
-                       ? amp_sin_acc(reduce_signed(x), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
-                       : fmaf(sin_slow(x), c1.z, acc[s]);
+          const float x = w[s] * c.x;
+          acc[s] = fmaf(fabsf(x) < kFastArgLimit ? sin_reduced(x) : sin_slow(x), c.y, acc[s]);
         }
       }
     }
@@ -483,7 +479,7 @@ int ddsp_hip_harmonic_synth_frames(const float* f0, const float* amplitudes, flo
   if (!f0 || !amplitudes || !distribution || !out) return DDSP_HIP_EINVAL;
   if (frames > INT32_MAX || batch > 65535 || n_harmonic > 8192 || block_size > (1 << 20))
     return DDSP_HIP_EINVAL;
-  const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
+  const size_t shm = sizeof(float2) * (size_t)((n_harmonic + 3) & ~3);
   launch_frames<false>(f0, amplitudes, distribution, write_back, out, batch, frames, n_harmonic,
                        block_size, sample_rate, shm, stream);
   return launch_status();
@@ -497,7 +493,7 @@ int ddsp_hip_harmonic_synth_params(const float* f0, const float* param, float* o
   if (!f0 || !param || !out) return DDSP_HIP_EINVAL;
   if (frames > INT32_MAX || batch > 65535 || n_harmonic > 8192 || block_size > (1 << 20))
     return DDSP_HIP_EINVAL;
-  const size_t shm = 2 * sizeof(float4) * (size_t)((n_harmonic + 3) & ~3);
+  const size_t shm = sizeof(float2) * (size_t)((n_harmonic + 3) & ~3);
   launch_frames<true>(f0, nullptr, const_cast<float*>(param), 0, out, batch, frames, n_harmonic,
                       block_size, sample_rate, shm, stream);
   return launch_status();

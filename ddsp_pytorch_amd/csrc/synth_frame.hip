@@ -2,10 +2,10 @@
 // workgroup: harmonic controls + oscillator bank (modules.py:44-80), noise controls + filter
 // design + filtered noise (modules.py:111-128), and `signal = harmonic + noise`.
 //
-// Why fuse: the oscillator bank is VALU-bound (12 VALU ops per sample x harmonic) while the
-// filtered-noise work is short, LDS- and latency-heavy phases.  In one kernel the noise phases
-// of some workgroups run beside the sine loops of others on the same CU, the harmonic signal
-// never makes an HBM round trip, and one launch replaces two.
+// Why fuse: the oscillator bank is VALU-bound (6 VALU ops + one hardware sine per sample x
+// harmonic) while the filtered-noise work is short, LDS- and latency-heavy phases.  In one
+// kernel the noise phases of some workgroups run beside the sine loops of others on the same
+// CU, the harmonic signal never makes an HBM round trip, and one launch replaces two.
 //
 // Mapping: thread t owns samples [4t, 4t+4) of the frame for both parts (bs <= 1024,
 // bs % 4 == 0), so the harmonic and noise values of a sample meet in registers.
@@ -35,8 +35,8 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   __shared__ double red[32];
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
-  float4* coef = smem4;                                   // [2*H4] float4
-  float* ct = reinterpret_cast<float*>(coef + 2 * H4);    // [n4]
+  float2* coef = reinterpret_cast<float2*>(smem4);       // [H4] (k+1, amplitude)
+  float* ct = reinterpret_cast<float*>(coef + H4);       // [n4]
   float* A = ct + n4;                                     // [NB -> 4]
   float* ir = A + ((NB + 3) & ~3);                        // [half+1 -> 4]
   float* h = ir + ((half + 4) & ~3);                      // [bs]
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
   for (int k = tid; k < H; k += NT) {  // modules.py:53-60 before normalisation
     const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
-    coef[2 * k].x = v;
+    coef[k].y = v;
     part_d += (double)v;
   }
   for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * NB + k] + bias);  // modules.py:113
@@ -86,9 +86,8 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
 
   // ---- phase 2: harmonic coefficient table; even half of the noise filter taps ----
   for (int k = tid; k < H4; k += NT) {
-    const float v = k < H ? (coef[2 * k].x / norm) * a : 0.0f;  // (dist / sum) * amp
-    coef[2 * k] = make_float4(v, v * kS3, v * kS5, v * kS7);
-    coef[2 * k + 1] = make_float4(v * kS9, (float)(k + 1), v, 0.0f);
+    const float v = k < H ? (coef[k].y / norm) * a : 0.0f;  // (dist / sum) * amp
+    coef[k] = make_float2((float)(k + 1), v);
   }
   if (n == 128 && NT >= 128) {
     if (tid < 64) {
@@ -140,22 +139,19 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
     }
     if (active) {
       if (fast) {
-#pragma unroll 2
+#pragma unroll 4
         for (int k = 0; k < H4; ++k) {
-          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+          const float2 c = coef[k];
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc[s] = amp_sin_acc(reduce_signed(w[s] * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s]);
+          for (int s = 0; s < 4; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
         }
       } else {
         for (int k = 0; k < H; ++k) {
-          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
+          const float2 c = coef[k];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            const float xx = w[s] * c1.y;
-            acc[s] = fabsf(xx) < kFastArgLimit
-                         ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, acc[s])
-                         : fmaf(sin_slow(xx), c1.z, acc[s]);
+            const float xx = w[s] * c.x;
+            acc[s] = fmaf(fabsf(xx) < kFastArgLimit ? sin_reduced(xx) : sin_slow(xx), c.y, acc[s]);
           }
         }
       }
@@ -171,15 +167,14 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
       float a = 0.0f;
       if (fabsf(wj) * (float)H4 < kFastArgLimit) {
         for (int k = 0; k < H4; ++k) {
-          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
-          a = amp_sin_acc(reduce_signed(wj * c1.y), c0.x, c0.y, c0.z, c0.w, c1.x, a);
+          const float2 c = coef[k];
+          a = fmaf(sin_reduced(wj * c.x), c.y, a);
         }
       } else {
         for (int k = 0; k < H; ++k) {
-          const float4 c0 = coef[2 * k], c1 = coef[2 * k + 1];
-          const float xx = wj * c1.y;
-          a = fabsf(xx) < kFastArgLimit ? amp_sin_acc(reduce_signed(xx), c0.x, c0.y, c0.z, c0.w, c1.x, a)
-                                        : fmaf(sin_slow(xx), c1.z, a);
+          const float2 c = coef[k];
+          const float xx = wj * c.x;
+          a = fmaf(fabsf(xx) < kFastArgLimit ? sin_reduced(xx) : sin_slow(xx), c.y, a);
         }
       }
       hsum[j] = a;
@@ -244,7 +239,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   }
   const int pad = (lo_end + 4 + 3) & ~3;
   const int H4 = ((int)n_harmonic + 3) & ~3, n4 = (n + 3) & ~3;
-  const size_t floats = (size_t)8 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs +
+  const size_t floats = (size_t)2 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs +
                         ((half + 3) & ~3) + pad + bs;
   if (sizeof(float) * floats > 120 * 1024) return DDSP_HIP_ERANGE;
   const int nt = std::max(64, ((bs / 4 + 63) / 64) * 64);
