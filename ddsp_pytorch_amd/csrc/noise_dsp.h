@@ -73,15 +73,21 @@ static __device__ __forceinline__ float ir_at(const float* ir, const float* ct, 
 
 // Truncated causal convolution y[j] = sum_{m<=j} h[m] x[j-m] for j in [j0, j0+4).
 // x points at a buffer with >= len4 zeros to the left of x[0]; h is zero outside its support.
-// Taps are visited in [0, lo_end) and [hi_start, len4), both multiples of 4.
+// Taps are visited in [0, lo_end) and [hi_start, len4), both multiples of 4.  h and x are
+// 16-B aligned and j0 % 4 == 0: every load is one ds_read_b128 (indexing in float4 units keeps
+// that visible to the compiler; with float offsets it split them into ds_read2_b32 pairs,
+// whose 16-B lane stride conflicts in the LDS banks).
 static __device__ __forceinline__ float4 fir4(const float* __restrict__ h, const float* __restrict__ x,
                                       int j0, int lo_end, int hi_start, int len4) {
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+  const float4* __restrict__ h4 = reinterpret_cast<const float4*>(h);
+  const int q0 = j0 >> 2;
   float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
   auto run = [&](int m_begin, int m_end) {
-    float4 cur = *reinterpret_cast<const float4*>(x + j0 - m_begin);  // x[j0-m .. j0-m+3]
-    for (int m = m_begin; m < m_end; m += 4) {
-      const float4 prv = *reinterpret_cast<const float4*>(x + j0 - m - 4);  // x[j0-m-4 .. j0-m-1]
-      const float4 hh = *reinterpret_cast<const float4*>(h + m);
+    float4 cur = x4[q0 - (m_begin >> 2)];  // x[j0-m .. j0-m+3]
+    for (int m4 = m_begin >> 2; m4 < (m_end >> 2); ++m4) {
+      const float4 prv = x4[q0 - m4 - 1];  // x[j0-m-4 .. j0-m-1]
+      const float4 hh = h4[m4];
       // tap m+d contributes h[m+d] * x[j0+r-m-d]
       y0 = fmaf(hh.x, cur.x, y0); y1 = fmaf(hh.x, cur.y, y1); y2 = fmaf(hh.x, cur.z, y2); y3 = fmaf(hh.x, cur.w, y3);
       y0 = fmaf(hh.y, prv.w, y0); y1 = fmaf(hh.y, cur.x, y1); y2 = fmaf(hh.y, cur.y, y2); y3 = fmaf(hh.y, cur.z, y3);

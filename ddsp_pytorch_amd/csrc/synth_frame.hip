@@ -112,7 +112,12 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   __syncthreads();
 
   // ---- phase 3: rolled/windowed filter h (core.py:158-164) ----
-  for (int j = tid; j < bs; j += NT) h[j] = ir_at_half(ir, ct, n, bs, j);
+  // only the taps the FIR reads: [0, lo_end) and [tail_start, bs) (the rest are zero)
+  const int nlo = lo_end, ntaps = lo_end + (bs - tail_start);
+  for (int i = tid; i < ntaps; i += NT) {
+    const int j = i < nlo ? i : tail_start + (i - nlo);
+    h[j] = ir_at_half(ir, ct, n, bs, j);
+  }
   __syncthreads();
 
   // ---- phase 4: noise tail (taps past bs - n/2 reach only the last n/2 outputs) ----

@@ -1,6 +1,6 @@
 """Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
 
-    python tools/kernel_probe.py {harmonic,harmonic_frames,noise,reverb,op} [reps]
+    python tools/kernel_probe.py {fused,harmonic,harmonic_frames,noise,reverb,op} [reps]
 """
 import os
 import sys
@@ -26,7 +26,9 @@ def main():
             f0s = core.upsample(inp["f0"], bs)
             a = core.upsample(dist, bs)
         for _ in range(reps):
-            if which == "harmonic":
+            if which == "fused":
+                core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr)
+            elif which == "harmonic":
                 core.harmonic_synth_params(inp["f0"], inp["param"], bs, sr)
             elif which == "harmonic_frames":
                 core.harmonic_synth_frames(inp["f0"], amps, dist, bs, sr, write_back=False)

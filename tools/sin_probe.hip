@@ -1,6 +1,8 @@
 // Probe: accuracy and throughput of sine evaluation variants on gfx950 for the oscillator bank.
 //   0: reduce_signed + amp-folded odd minimax polynomial (amp_sin_acc)      [12 VALU]
 //   1: Cody-Waite by 2pi in radians, scale to revolutions, hardware v_sin_f32
+//   3, 4: 2 of 4 / 3 of 4 samples on variant 2, the rest on variant 0 (does the transcendental
+//      unit issue beside the VALU?); 5: bare v_sin + fma (transcendental rate)
 //   2: reduction directly in revolutions (two-term 1/(2pi) by fma), hardware v_sin_f32 [shipped:
 //      common.h reduce_rev + sin_rev]
 // Accuracy vs fp64 sin of the same fp32 argument (|x| < kFastArgLimit); throughput in a
@@ -60,7 +62,16 @@ __global__ void bench(float* out, const float* amp, float w0, int H) {
       const float x = w[s] * kk;
       if (V == 0) acc[s] = amp_sin_acc(reduce_signed(x), a, c[1], c[2], c[3], c[4], acc[s]);
       else if (V == 1) acc[s] = fmaf(sin_hw1(x), a, acc[s]);
-      else acc[s] = fmaf(sin_hw2(x), a, acc[s]);
+      else if (V == 2) acc[s] = fmaf(sin_hw2(x), a, acc[s]);
+      else if (V == 3) {  // mixed: two samples on the hardware sine, two on the polynomial
+        if (s < 2) acc[s] = fmaf(sin_hw2(x), a, acc[s]);
+        else acc[s] = amp_sin_acc(reduce_signed(x), a, c[1], c[2], c[3], c[4], acc[s]);
+      } else if (V == 4) {  // mixed 3:1
+        if (s < 3) acc[s] = fmaf(sin_hw2(x), a, acc[s]);
+        else acc[s] = amp_sin_acc(reduce_signed(x), a, c[1], c[2], c[3], c[4], acc[s]);
+      } else {  // transcendental rate: v_sin + one fma
+        acc[s] = fmaf(__builtin_amdgcn_sinf(x), a, acc[s]);
+      }
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
@@ -101,12 +112,15 @@ int main() {
   hipMemcpy(damp, hamp.data(), 128 * 8 * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const int H = 400, blocks = 25600;
-  for (int v = 0; v < 3; ++v) {
+  for (int v = 0; v < 6; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       hipEventRecord(e0);
       if (v == 0) hipLaunchKernelGGL(bench<0>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
       else if (v == 1) hipLaunchKernelGGL(bench<1>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
-      else hipLaunchKernelGGL(bench<2>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
+      else if (v == 2) hipLaunchKernelGGL(bench<2>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
+      else if (v == 3) hipLaunchKernelGGL(bench<3>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
+      else if (v == 4) hipLaunchKernelGGL(bench<4>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
+      else hipLaunchKernelGGL(bench<5>, dim3(blocks), dim3(128), 0, 0, dout, damp, 0.05f, H);
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       if (rep == 3)
