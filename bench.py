@@ -35,8 +35,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3   # vector / f32-MFMA peak
 VALU_PEAK_LANE_OPS = 256 * 128 * 2.4e9  # 256 CUs x 128 fp32 lanes/clk x 2.4 GHz (= 157.3 TF / 2)
-OSC_VALU_SLOTS = 8         # VALU issue slots per (sample, harmonic) in the oscillator's inner loop:
-                           # 6 VALU ops + one v_sin_f32 (8-cycle issue = 2 slots)
+OSC_VALU_SLOTS = 9         # VALU issue slots per (sample, harmonic) in the oscillator's inner loop:
+                           # 6 VALU ops + one v_sin_f32, which costs ~3 slots (tools/sin_probe.hip:
+                           # the same loop with 12 VALU ops, with 6 + v_sin and with 2 + v_sin)
 
 
 def parse():
@@ -411,8 +412,8 @@ def main():
                               "kernel; it physically reads only frame-rate controls",
                 "sines_per_s": round(n_sin / (osc_ms * 1e-3), 1),
                 "valu_frac": round(n_sin * OSC_VALU_SLOTS / (osc_ms * 1e-3) / VALU_PEAK_LANE_OPS, 4),
-                "valu_note": "the fused kernel is VALU-bound: valu_frac = sines/s x 8 VALU issue slots "
-                             "per (sample, harmonic: 6 VALU ops + one hardware sine at 2 slots) / "
+                "valu_note": "the fused kernel is VALU-bound: valu_frac = sines/s x 9 VALU issue slots "
+                             "per (sample, harmonic: 6 VALU ops + one hardware sine at ~3 slots) / "
                              "(256 CU x 128 lanes x 2.4 GHz); the noise FIR and controls in the same "
                              "launch are not counted"}
 

@@ -93,10 +93,10 @@ __device__ __forceinline__ float reduce_rev(float x) {
   return fmaf(x, kInv2PiLo, y);
 }
 
-// sin(2*pi*y) on the hardware sine (v_sin_f32 takes revolutions; one transcendental issue,
-// ~2 VALU slots).  With reduce_rev: |error| < 3.2e-7, rms 5.3e-8 vs the fp64 sine of the same
+// sin(2*pi*y) on the hardware sine (v_sin_f32 takes revolutions; it costs ~3 VALU issue
+// slots, measured).  With reduce_rev: |error| < 3.2e-7, rms 5.3e-8 vs the fp64 sine of the same
 // fp32 argument over |x| < 7.9e6 (tools/sin_probe.hip on MI355X), against the polynomial's
-// 1.8e-7 / 3.5e-8 — and 1.44x its throughput (8 VALU slots per sine instead of 12).
+// 1.8e-7 / 3.5e-8 — at 1.35-1.44x its measured throughput (~9 slots per sine instead of 12).
 __device__ __forceinline__ float sin_rev(float y) { return __builtin_amdgcn_sinf(y); }
 
 // sin(x) for |x| < kFastArgLimit.
