@@ -385,17 +385,22 @@ def main():
         elapsed = float(t.item())
     assert torch.isfinite(out).all()
 
-    breakdown = EventTimer(["synth_frames", "reverb"])
-    syn.timer = breakdown
-    breakdown.enabled = True
-    for _ in range(min(args.steps, 20)):
-        step()
-    torch.cuda.synchronize()
-    breakdown.enabled = False
+    # per-kernel breakdown: one event pair per step, one kernel group per loop (events around
+    # every group of a step add their own gaps and read high against rocprofv3)
+    kern_ms = {}
+    for name in ("synth_frames", "reverb"):
+        breakdown = EventTimer([name])
+        syn.timer = breakdown
+        breakdown.enabled = True
+        for _ in range(min(args.steps, 50)):
+            step()
+        torch.cuda.synchronize()
+        breakdown.enabled = False
+        kern_ms[name] = breakdown.mean_ms(name)
+    syn.timer = None
 
     samples_per_step = B * F * bs * world
     value = samples_per_step * args.steps / elapsed
-    kern_ms = {n: breakdown.mean_ms(n) for n in breakdown.names}
     traffic = load_traffic(args.traffic)
 
     # dominant kernel: fused oscillator (per-launch = B*F*bs samples of this rank)
@@ -429,6 +434,9 @@ def main():
                    "global_batch": B * world, "seq_len": F * bs, "parallelism": f"batch-shard x{world}"},
         "roofline": roofline,
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
+        "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region "
+                          "(the VALU-bound synthesis kernel runs up to ~20% slower once the device "
+                          "is hot; roofline.avg_launch_ms is from inside the timed region)",
     }
 
     if dist and not args.no_gather:
