@@ -1,6 +1,11 @@
-"""Steady-state time of the fused synthesis kernel at config 2 (library chosen by DDSP_HIP_LIB):
-A/B experiments on kernel variants.   python tools/exp_synth_time.py [H ...]"""
+"""Time the fused synthesis kernel (core.synth_frames) at config 2 after the device has
+settled: median of several event-timed groups (development experiment for launch-shape
+variants selected through environment variables read by the library).
+
+    python tools/exp_synth_time.py [batch frames harmonics]
+"""
 import os
+import statistics
 import sys
 import time
 
@@ -10,18 +15,29 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddsp_pytorch_amd import core  # noqa: E402
 from ddsp_pytorch_amd.synth import make_inputs  # noqa: E402
 
-B, F, bs, sr = 64, 200, 512, 48000
-for H in [int(a) for a in sys.argv[1:]] or [100]:
-    inp = make_inputs(B, F, H, 65, bs, device="cuda", with_noise=False)
-    fn = lambda: core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr)
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 0.3:
-        fn()
-        torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(200):
-        fn()
-    e1.record()
+
+def main():
+    B, F, H = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (64, 200, 100)))
+    NB, bs, sr = 65, 512, 48000
+    inp = make_inputs(B, F, H, NB, bs, device="cuda", with_noise=False)
+    run = lambda: core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr)
+    t = time.perf_counter()
+    while time.perf_counter() - t < 0.5:
+        run()
     torch.cuda.synchronize()
-    print(f"{os.environ.get('DDSP_HIP_LIB', 'default')} H={H} synth_frames {e0.elapsed_time(e1) / 200 * 1e3:.1f} us", flush=True)
+    groups = []
+    for _ in range(7):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        groups.append(e0.elapsed_time(e1) / 20)
+    env = {k: v for k, v in os.environ.items() if k.startswith("DDSP_HIP_")}
+    print(f"{env} B={B} F={F} H={H}: median {statistics.median(groups) * 1e3:.1f} us "
+          f"(min {min(groups) * 1e3:.1f}, max {max(groups) * 1e3:.1f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
