@@ -19,13 +19,15 @@ else:
     out = core.filtered_noise(mags, bs, raw_bias=-5.0)
 def bwd():
     out.backward(g, retain_graph=True)
-for _ in range(3):
+import time
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < 0.5:  # clocks / power state settle
     bwd()
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-for _ in range(20):
+for _ in range(50):
     bwd()
 e1.record()
 torch.cuda.synchronize()
-print(json.dumps({"mode": mode, "threads": os.environ.get("DDSP_HIP_BWD_THREADS", "default"), "ms": round(e0.elapsed_time(e1) / 20, 4)}))
+print(json.dumps({"mode": mode, "threads": os.environ.get("DDSP_HIP_BWD_THREADS", "default"), "ms": round(e0.elapsed_time(e1) / 50, 4)}))
