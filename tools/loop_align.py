@@ -15,6 +15,7 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
 def analyze(so, kern="synth_frame_kernelILb1ELb0EE"):
+    """the kernel's sine loop: start address, size, 8-byte instructions at odd dword addresses"""
     tmp = tempfile.mkdtemp()
     local = os.path.join(tmp, os.path.basename(so))
     shutil.copy(so, local)
@@ -36,15 +37,33 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0EE"):
     for l in out:
         m=re.search(r"//\s*([0-9A-F]+):\s*((?:[0-9A-F]{8}\s*)+)",l)
         if m: ins.append((int(m.group(1),16), len(m.group(2).split())*4, l.split("//")[0].strip()))
-    # loop: find first ds_read_b128 v[0:3], v4 ; start = previous instr
-    idx=[i for i,x in enumerate(ins) if x[2].startswith("ds_read_b128 v[0:3], v4") and "offset" not in x[2]][0]-1
-    start=ins[idx][0]
-    end=[i for i,x in enumerate(ins[idx:]) if x[2].startswith("s_cbranch_scc0")][0]+idx
-    body=ins[idx:end+1]
+    # the hot loop: the innermost backward-branch loop holding >= 8 v_sin_f32
+    best = None
+    for i, (addr, size, txt) in enumerate(ins):
+        m = re.match(r"s_cbranch_\w+\s+(-?\d+)", txt)
+        if not m:
+            continue
+        target = addr + 4 + 4 * int(m.group(1)) if int(m.group(1)) < 32768 else addr + 4 + 4 * (int(m.group(1)) - 65536)
+        if target >= addr:
+            continue
+        body = [x for x in ins if target <= x[0] <= addr]
+        nsin = sum(1 for x in body if x[2].startswith("v_sin_f32"))
+        # innermost: the smallest body with at least 8 sines
+        if nsin >= 8 and (best is None or len(body) < len(best[2])):
+            best = (nsin, target, body)
+    if best is None:
+        print(f"{so}: no sine loop in {kern}")
+        return
+    _, start, body = best
     eight=[x for x in body if x[1]==8]
     mis=[x for x in eight if x[0]%8!=0]
-    print(f"{so.split('/')[-1]}: loop @{start:#x} (mod 8 = {start%8}), {len(body)} instrs, {sum(x[1] for x in body)} B, 8-byte {len(eight)}, misaligned {len(mis)}")
+    print(f"{so.split('/')[-1]} {kern}: loop @{start:#x} (mod 8 = {start%8}), {len(body)} instrs, {sum(x[1] for x in body)} B, 8-byte {len(eight)}, misaligned {len(mis)}")
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for so in sys.argv[1:] or [os.path.join(root, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")]:
-        analyze(so)
+    libs = [a for a in sys.argv[1:] if a.endswith(".so")] or [
+        os.path.join(root, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")]
+    kerns = [a for a in sys.argv[1:] if not a.endswith(".so")] or [
+        "synth_frame_kernelILb1ELb0EE", "frame_backward_kernelILi2ELi2ELb1EE"]
+    for so in libs:
+        for k in kerns:
+            analyze(so, k)
