@@ -231,6 +231,9 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
 #pragma unroll
         for (int c = 0; c < kKPT; ++c) acc2[c] = 0.0f;
         int j = j0;
+        // loop placement (tools/loop_align.py): one dword of padding puts this
+        // instantiation's 8-byte instructions at odd dword addresses, as the others already are
+        if constexpr (HMODE == 1 && NOISE == 0) asm volatile("s_nop 0");
         for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
           const float2 p = wg[j], p1 = wg[j + 1];
           // the 8 chains written stage by stage so the scheduler keeps them interleaved (ILP 8)

@@ -142,6 +142,10 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
       acc[s] = 0.0f;
       fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
     }
+    // loop placement: the sine loop runs ~10% faster when its 8-byte instructions sit at odd dword
+    // addresses (tools/loop_align.py); the injected-noise instantiation needs one
+    // dword of padding ahead of it to get there
+    if constexpr (!RNG) asm volatile("s_nop 0");
     if (active) {
       if (fast) {
 #pragma unroll 4

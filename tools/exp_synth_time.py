@@ -2,7 +2,7 @@
 settled: median of several event-timed groups (development experiment for launch-shape
 variants selected through environment variables read by the library).
 
-    python tools/exp_synth_time.py [batch frames harmonics]
+    python tools/exp_synth_time.py [batch frames harmonics]     (DDSP_AB_INJECT=1: injected noise)
 """
 import os
 import statistics
@@ -19,8 +19,9 @@ from ddsp_pytorch_amd.synth import make_inputs  # noqa: E402
 def main():
     B, F, H = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (64, 200, 100)))
     NB, bs, sr = 65, 512, 48000
-    inp = make_inputs(B, F, H, NB, bs, device="cuda", with_noise=False)
-    run = lambda: core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr)
+    inject = os.environ.get("DDSP_AB_INJECT") == "1"
+    inp = make_inputs(B, F, H, NB, bs, device="cuda", with_noise=inject)
+    run = lambda: core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr, noise=inp.get("noise"))
     t = time.perf_counter()
     while time.perf_counter() - t < 0.5:
         run()
