@@ -2,7 +2,8 @@
 settled: median of several event-timed groups (development experiment for launch-shape
 variants selected through environment variables read by the library).
 
-    python tools/exp_synth_time.py [batch frames harmonics]     (DDSP_AB_INJECT=1: injected noise)
+    python tools/exp_synth_time.py [batch frames harmonics]     (DDSP_AB_INJECT=1: injected noise;
+                                                                 DDSP_AB_WHAT=reverb: the 1 s reverb)
 """
 import os
 import statistics
@@ -22,6 +23,12 @@ def main():
     inject = os.environ.get("DDSP_AB_INJECT") == "1"
     inp = make_inputs(B, F, H, NB, bs, device="cuda", with_noise=inject)
     run = lambda: core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr, noise=inp.get("noise"))
+    if os.environ.get("DDSP_AB_WHAT") == "reverb":
+        from ddsp_pytorch_amd.synth import SynthPath
+        rv = SynthPath(bs, sr, reverb_length=48000).to("cuda").reverb
+        sig = run()
+        spec = rv._spectrum(F * bs)
+        run = lambda: core.reverb_apply(sig, spec, rv.length)
     t = time.perf_counter()
     while time.perf_counter() - t < 0.5:
         run()
