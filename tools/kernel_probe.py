@@ -1,6 +1,6 @@
 """Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
 
-    python tools/kernel_probe.py {fused,harmonic,harmonic_frames,noise,reverb,op} [reps]
+    python tools/kernel_probe.py {fused,bwd,harmonic,harmonic_frames,noise,reverb,op} [reps]
 """
 import os
 import sys
@@ -19,6 +19,15 @@ def main():
     B, F, H, NB, bs, sr = 64, 200, 100, 65, 512, 48000
     inp = make_inputs(B, F, H, NB, bs, seed=0, device=dev, with_noise=False)
     syn = SynthPath(bs, sr, reverb_length=48000).to(dev)
+    if which == "bwd":  # the fused synthesis backward (frame_backward_kernel<2, 2, true>)
+        param = inp["param"].clone().requires_grad_(True)
+        mags = inp["mags"].clone().requires_grad_(True)
+        out = core.synth_frames(inp["f0"], param, mags, bs, sr)
+        g = torch.randn_like(out)
+        for _ in range(reps):
+            out.backward(g, retain_graph=True)
+        torch.cuda.synchronize()
+        return
     with torch.no_grad():
         amps, dist = core.harmonic_controls(inp["param"][..., :1], inp["param"][..., 1:], inp["f0"], sr)
         x = torch.randn(B, F * bs, 1, device=dev)
