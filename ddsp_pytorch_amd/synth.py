@@ -72,6 +72,77 @@ class SynthPath(nn.Module):
         return signal
 
 
+class SynthGraph:
+    """A fixed-shape SynthPath step captured into one HIP graph (torch.cuda.CUDAGraph is hipGraph
+    on ROCm) and replayed per call: the serving form of the path for a batch whose shape does not
+    change (SURVEY.md §8(b) asks for HIP streams and graphs instead of a tracing compiler).
+
+    The graph holds the fused synthesis kernel and the reverb's three UPOLS kernels; replay
+    launches them back to back with no host work between them.  Inputs are the static tensors
+    given here (update them in place between replays); ``out`` is a static buffer overwritten by
+    every replay.
+
+    * Device noise (``noise=None``): drawn with the offset held in the device counter ``counter``
+      (``ddsp_hip_synth_frames_counter``), advanced on the stream by every replay — replay k draws
+      the noise of ``core.synth_frames`` at offset k (parity: tests/test_gpu_device_noise.py).
+    * ``rebuild_ir=True`` also captures ``Reverb.build_impulse`` and the IR spectrum
+      (modules.py:30-33 rebuilds them on every forward); by default the spectrum cached by the
+      module (``Reverb._spectrum``) is captured, so re-capture after changing the reverb's
+      parameters.
+    """
+
+    def __init__(self, path, f0, param, mags, noise=None, seed=0x5EEDDD5B, rebuild_ir=False, warmup=2):
+        if f0.device.type != "cuda":
+            raise RuntimeError("SynthGraph: inputs must be on a HIP device")
+        self.path = path
+        self.f0, self.param, self.mags, self.noise = f0, param, mags, noise
+        self.seed = int(seed)
+        self.rebuild_ir = bool(rebuild_ir)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=f0.device)
+        if noise is None and not core.synth_frames_in_envelope(param.shape[-1] - 1, mags.shape[-1],
+                                                               path.block_size, param.shape[0]):
+            raise RuntimeError("SynthGraph: device noise needs the fused kernel's shape envelope")
+        self.graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(f0.device)
+        side.wait_stream(torch.cuda.current_stream(f0.device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(max(1, int(warmup))):  # workspaces and library state before capture
+                self._step()
+        torch.cuda.current_stream(f0.device).wait_stream(side)
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = self._step()
+        self.reset()
+
+    def _step(self):
+        p = self.path
+        if self.noise is None:
+            sig = core.synth_frames_counter(self.f0, self.param, self.mags, p.block_size, p.sample_rate,
+                                            self.counter, self.seed, bias=p.initial_bias)
+        else:
+            sig = core.synth_frames(self.f0, self.param, self.mags, p.block_size, p.sample_rate,
+                                    bias=p.initial_bias, noise=self.noise)
+            if sig is None:
+                harmonic = core.harmonic_synth_params(self.f0, self.param, p.block_size, p.sample_rate)
+                sig = core.filtered_noise(self.mags, p.block_size, noise=self.noise, add=harmonic,
+                                          raw_bias=p.initial_bias)
+        rv = p.reverb
+        if rv is None:
+            return sig
+        if self.rebuild_ir:
+            spec = core.reverb_spectrum(rv.build_impulse(), sig.shape[1])
+        else:
+            spec = rv._spectrum(sig.shape[1])
+        return core.reverb_apply(sig, spec, rv.length)
+
+    def reset(self):
+        """Rewind the device-noise counter (the next replay draws offset 0)."""
+        self.counter.zero_()
+
+    def replay(self):
+        self.graph.replay()
+        return self.out
+
+
 class _Null:
     def __enter__(self):
         return self

@@ -136,3 +136,68 @@ def multiscale_spec_loss(ori_stft, rec_stft):
     for s_x, s_y in zip(ori_stft, rec_stft):
         loss = loss + (s_x - s_y).abs().mean() + (safe_log(s_x) - safe_log(s_y)).abs().mean()
     return loss
+
+
+# ---------------------------------------------------------------- the control network (decoder.py)
+# Restated over a plain state_dict (the reference's keys), so the checker shares no code with
+# the product's modules.
+
+def mlp_forward(sd, prefix, x):
+    # ddsp/core.py:122-129: (Linear, LayerNorm, LeakyReLU) x 3 -> Sequential indices 0..8
+    for i in (0, 3, 6):
+        x = F.linear(x, sd[f"{prefix}.{i}.weight"], sd[f"{prefix}.{i}.bias"])
+        x = F.layer_norm(x, (x.shape[-1],), sd[f"{prefix}.{i + 1}.weight"], sd[f"{prefix}.{i + 1}.bias"])
+        x = F.leaky_relu(x)
+    return x
+
+
+def gru_forward(sd, prefix, x, h0):
+    # ddsp/core.py:132-133: nn.GRU(2 * hidden, hidden, batch_first=True) — torch's CPU GRU
+    hidden = sd[f"{prefix}.weight_hh_l0"].shape[1]
+    g = torch.nn.GRU(x.shape[-1], hidden, batch_first=True)
+    g.load_state_dict({k: sd[f"{prefix}.{k}"] for k in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0",
+                                                         "bias_hh_l0")})
+    return g(x, h0) if h0 is not None else g(x)
+
+
+def gru_decoder_forward(sd, f0, loudness, cache=None):
+    """ddsp/models/decoder.py:43-68 (z_dim=None).  With ``cache`` ([1,1,hidden], updated in
+    place) the realtime branch of decoder.py:56-60: the GRU starts from and writes back the
+    cached state."""
+    hidden = torch.cat([mlp_forward(sd, "decoder.f0_mlp", f0), mlp_forward(sd, "decoder.loudness_mlp", loudness)],
+                       -1)
+    if cache is not None:
+        gru_out, h = gru_forward(sd, "decoder.gru", hidden, cache)
+        cache.copy_(h)
+    else:
+        gru_out = gru_forward(sd, "decoder.gru", hidden, None)[0]
+    return mlp_forward(sd, "decoder.out_mlp", torch.cat([gru_out, f0, loudness], -1))
+
+
+@torch.no_grad()
+def decoder_synthesis(sd, f0, hidden, noise, block_size, sample_rate, reverb=None):
+    """ddsp/models/decoder.py:106-125 (and realtime_forward, decoder.py:138-158, with reverb=None):
+    projections, both synths with injected noise, the sum, the optional reverb.  Returns
+    (signal, harmonic, filtered noise)."""
+    param = F.linear(hidden, sd["harmonic_proj.weight"], sd["harmonic_proj.bias"])
+    amp, dist = harmonic_controls(param[..., :1], param[..., 1:], f0, sample_rate)
+    harmonic = harmonic_forward(amp, dist, f0, block_size, sample_rate)
+    mags = scale_function(F.linear(hidden, sd["noise_proj.weight"], sd["noise_proj.bias"]) + (-5.0))
+    noise_audio = noise_forward(mags, noise, block_size)
+    signal = harmonic + noise_audio
+    if reverb is not None:
+        signal = reverb(signal)
+    return signal, harmonic, noise_audio
+
+
+@torch.no_grad()
+def realtime_forward(sd, pitch, loudness, mean, std, cache, noise, block_size, sample_rate):
+    """export.py:33-40 ScriptDDSP.forward with realtime=True on a [1, N, 1] call: loudness
+    normalised, both inputs decimated by block_size ([:, ::block_size]), GRU on the cached
+    state (decoder.py:56-60, ``cache`` updated in place), harmonic + noise, no reverb
+    (decoder.py:138-158).  ``noise`` is the call's [1, N / block_size, block_size] U[-1,1)."""
+    loudness = (loudness - mean) / std
+    pitch = pitch[:, ::block_size]
+    loudness = loudness[:, ::block_size]
+    hidden = gru_decoder_forward(sd, pitch, loudness, cache)
+    return decoder_synthesis(sd, pitch, hidden, noise, block_size, sample_rate)[0]

@@ -192,6 +192,45 @@ def main():
          magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
 
     grad_goldens(ddsp, decoder, modules, sr)
+    realtime_goldens(decoder, sr)
+
+
+@torch.no_grad()
+def realtime_goldens(decoder, sr):
+    # ---------------- g8: the realtime stream (config 3) ----------------
+    # export.py:33-40 ScriptDDSP.forward(realtime=True) on successive 1024-sample calls: loudness
+    # normalised with the stored mean/std, pitch and loudness decimated by block_size, then the
+    # model's realtime_forward (decoder.py:138-158).  That method reads `self.proj_matrices`, which
+    # the fork's DDSPDecoder never defines; the projections it names are
+    # harmonic_proj / noise_proj (decoder.py:87-88), used here.  Everything else is the
+    # reference's own modules: GRUDecoder.forward(realtime=True) carrying cache_gru
+    # (decoder.py:56-60), HarmonicSynth, FilteredNoise (its torch.rand draw seeded per call).
+    bs, H, N, mean, std = 256, 64, 1024, -3.0, 1.5
+    torch.manual_seed(0)
+    model = decoder.DDSPDecoder(64, H, 65, sr, bs, False).eval()
+    g = torch.Generator().manual_seed(18)
+    model.decoder.cache_gru.copy_(torch.randn(1, 1, 64, generator=g) * 0.1)
+    sd = {"sd." + k: v.clone() for k, v in model.state_dict().items()}
+    calls = {}
+    for k in range(3):
+        pitch = 80.0 * 10.0 ** torch.rand(1, N, 1, generator=g)
+        loud = torch.randn(1, N, 1, generator=g) - 2.0
+        p = pitch[:, ::bs]
+        lo = ((loud - mean) / std)[:, ::bs]
+        hidden = model.decoder(p, lo, realtime=True)
+        param = model.harmonic_proj(hidden)
+        hc = model.harmonic_synth.get_controls(param[..., :1], param[..., 1:], p)
+        harmonic = model.harmonic_synth(**hc)
+        nc = model.noise_synth.get_controls(model.noise_proj(hidden))
+        torch.manual_seed(200 + k)
+        noise_in = torch.rand(1, N // bs, bs) * 2 - 1  # the draw FilteredNoise.forward makes next
+        torch.manual_seed(200 + k)
+        noise = model.noise_synth(**nc)
+        calls.update({f"pitch_{k}": pitch, f"loudness_{k}": loud, f"noise_in_{k}": noise_in,
+                      f"signal_{k}": harmonic + noise, f"harmonic_{k}": harmonic,
+                      f"cache_{k}": model.decoder.cache_gru.clone()})
+    save("g8_realtime", hidden_size=64, n_harmonic=H, n_bands=65, sample_rate=sr, block_size=bs,
+         mean_loudness=mean, std_loudness=std, noise_seeds=np.array([200, 201, 202]), **calls, **sd)
 
 
 @torch.enable_grad()
@@ -250,4 +289,8 @@ def grad_goldens(ddsp, decoder, modules, sr):
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["g8"]:  # only the realtime fixture
+        torch.set_num_threads(8)
+        realtime_goldens(import_reference()[2], 48000)
+    else:
+        main()

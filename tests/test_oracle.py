@@ -102,3 +102,36 @@ def test_synth_path_decoder_golden():
     f0 = g["pitch"]
     out, _ = no.harmonic_forward(g["amplitudes"], g["distribution"] / g["amplitudes"], f0, 512, 48000)
     assert rms(out, g["harmonic_audio"]) < 1e-6
+
+
+def _sd(g):
+    return {k[3:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("sd.")}
+
+
+def test_decoder_oracle_vs_golden():
+    """torch_ref's control network + synthesis restatement vs the reference's DDSPDecoder.forward."""
+    g = load_golden("g5_decoder")
+    sd = _sd(g)
+    f0, lo = T(g["pitch"]), T(g["loudness"])
+    with torch.no_grad():
+        hidden = tr.gru_decoder_forward(sd, f0, lo)
+        torch.manual_seed(123)
+        noise = torch.rand(1, 16, 512) * 2 - 1
+        rv = tr.Reverb(sd["reverb.noise"], sd["reverb.decay"], sd["reverb.wet"], 48000, 48000)
+        sig, harm, nz = tr.decoder_synthesis(sd, f0, hidden, noise, 512, 48000, rv)
+    assert torch.equal(harm, T(g["harmonic_audio"]))
+    assert torch.equal(nz, T(g["noise"]))
+    assert torch.equal(sig, T(g["signal"]))
+
+
+def test_realtime_oracle_vs_golden():
+    """export.py:33-40 realtime calls (decimation, loudness normalisation, cache_gru carried across
+    calls, decoder.py:56-60) restated in torch_ref vs the reference's modules (g8)."""
+    g = load_golden("g8_realtime")
+    sd = _sd(g)
+    cache = sd["decoder.cache_gru"].clone()
+    for k in range(3):
+        out = tr.realtime_forward(sd, T(g[f"pitch_{k}"]), T(g[f"loudness_{k}"]), float(g["mean_loudness"]),
+                                  float(g["std_loudness"]), cache, T(g[f"noise_in_{k}"]), 256, 48000)
+        assert torch.equal(out, T(g[f"signal_{k}"])), k
+        assert torch.equal(cache, T(g[f"cache_{k}"])), k
