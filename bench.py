@@ -12,14 +12,15 @@ each synthesising its own 64-item shard (batch items are independent — no coll
 the data path; weak scaling); the timed region is bracketed by barrier + synchronize and
 the max over ranks is reported.  Rank 0 prints ONE JSON line.
 
-Roofline: the oscillator's algorithmic bytes are 4*(H+2) B per output
-sample at its op boundary (f0 + H amplitudes in, 1 sample out).
-  * "roofline"    — the dominant kernel of the timed step, the fused frame-rate
-    oscillator, credited with those bytes (effective-bandwidth convention of §8(d); its
-    physical HBM traffic is only the waveform, see "traffic"), duration from HIP events
-    on its stream inside the timed region;
-  * "roofline_op" — the op-boundary harmonic_synth kernel (per-sample f0 [B,T,1] and
-    amplitudes [B,T,H] read from HBM), timed in a separate leg after the timed region.
+Rooflines:
+  * "roofline"    — the dominant kernel of the timed step, the fused synthesis kernel, against its
+    real bound, VALU issue: issue slots per launch (PMC instruction counts, the sine at 4 slots) /
+    launch duration (HIP events on its stream inside the timed region) / the chip's issue peak;
+    "traffic" is its PMC HBM bytes (it reads only frame-rate controls);
+  * "op_boundary_effective" — SURVEY.md §8(d)'s convention, the oscillator's op-boundary bytes
+    4*(H+2) B/sample divided by the fused kernel's time (not a roofline: fusion removed them);
+  * "roofline_op" — the op-boundary harmonic_synth kernel (per-sample f0 [B,T,1] and amplitudes
+    [B,T,H] read from HBM), HBM-bound, timed in a separate leg after the timed region.
 """
 import argparse
 import json
@@ -33,11 +34,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3   # vector / f32-MFMA peak
-VALU_PEAK_LANE_OPS = 256 * 128 * 2.4e9  # 256 CUs x 128 fp32 lanes/clk x 2.4 GHz (= 157.3 TF / 2)
-OSC_VALU_SLOTS = 9         # VALU issue slots per (sample, harmonic) in the oscillator's inner loop:
-                           # 6 VALU ops + one v_sin_f32, which costs ~3 slots (tools/sin_probe.hip:
-                           # the same loop with 12 VALU ops, with 6 + v_sin and with 2 + v_sin)
+# VALU issue model of gfx950, measured by tools/issue_probe.hip (profiles/r02_issue_probe.log): with
+# two or more waves per SIMD an fp32 VALU op (v_fma/v_mul/v_add) issues every ~2 cycles per SIMD
+# (2.26 at 8 waves/SIMD; 4-5 with a single wave, MI355X_MICROARCH.md's one-wave row), and the
+# transcendental v_sin_f32 every 8 cycles regardless of waves.  One issue SLOT = 2 SIMD cycles:
+# fp32 VALU op = 1 slot, v_sin_f32 = 4 slots.  Peak = 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles.
+VALU_PEAK_SLOTS = 256 * 4 * 2.4e9 / 2      # 1.2288e12 wave-instruction slots/s
+SIN_SLOTS = 4
+OSC_SLOTS_PER_SINE = 6 + SIN_SLOTS         # per (sample, harmonic): 6 fp32 VALU ops + one v_sin_f32
+                                           # (synth_frame.hip inner loop; tools/loop_align.py counts it)
 
 
 def parse():
@@ -78,6 +83,10 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC HBM bytes per launch (tools/pmc_traffic.py output)")
+    p.add_argument("--valu-counts", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
+                   help="PMC SQ_INSTS_VALU per launch of the dominant kernel (tools/pmc_valu.py output)")
+    p.add_argument("--no-uncached-leg", action="store_true",
+                   help="skip the step with the IR spectrum rebuilt on every call (as modules.py:30-33)")
     a = p.parse_args()
     cfg = {2: (64, 200, 100, 48000), 4: (16, 200, 100, 96000), 5: (64, 400, 128, 48000)}[a.config]
     if a.cpu_batch is None:
@@ -130,11 +139,20 @@ def load_traffic(path):
 
 def cpu_baseline(args, rank_inputs_seed=0):
     """The reference's algorithm on the host cores: oracle/torch_ref.py (the same ATen op
-    sequence as ddsp/core.py + modules.py, bit-exact to the reference's goldens)."""
+    sequence as ddsp/core.py + modules.py, bit-exact to the reference's goldens).
+
+    Thread counts (BASELINE.md's plan: torch.set_num_threads(os.cpu_count())): the sample is
+    timed at os.cpu_count() threads and at the process's CPU share (OMP_NUM_THREADS / the
+    affinity mask; a GPU box gives one process a 16-core share of a larger host), and the faster
+    of the two is reported, with both timings and the host's core count."""
     from oracle import torch_ref as tr
     from ddsp_pytorch_amd.synth import make_inputs
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    host = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = host
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
     B = args.cpu_batch
     inp = make_inputs(B, args.frames, args.harmonics, args.bands, args.block_size, seed=0)
     torch.manual_seed(1)
@@ -142,22 +160,32 @@ def cpu_baseline(args, rank_inputs_seed=0):
     rv = tr.Reverb(noise, torch.tensor(5.0), torch.tensor(0.0), args.reverb_length, args.sample_rate)
     run = lambda: tr.synth_path(inp["f0"], inp["param"], inp["mags"], inp["noise"], rv,
                                 args.block_size, args.sample_rate)
-    run()  # warm-up
-    times = []
-    budget = time.perf_counter() + 25.0
-    for _ in range(args.cpu_reps):
-        t0 = time.perf_counter()
-        run()
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() > budget:
-            break
-    t = sorted(times)[len(times) // 2]
     samples = B * args.frames * args.block_size
-    return {"value": samples / t, "unit": "samples/s", "cores": threads, "kind": "port",
+    timed = {}
+    prev = torch.get_num_threads()
+    for threads in sorted({host, share}):
+        torch.set_num_threads(threads)
+        run()  # warm-up
+        times = []
+        budget = time.perf_counter() + 15.0
+        for _ in range(args.cpu_reps):
+            t0 = time.perf_counter()
+            run()
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() > budget:
+                break
+        timed[threads] = (sorted(times)[len(times) // 2], len(times))
+    torch.set_num_threads(prev)
+    best = min(timed, key=lambda k: timed[k][0])
+    t, reps = timed[best]
+    return {"value": samples / t, "unit": "samples/s", "cores": best, "kind": "port",
+            "host_cpu_count": host, "affinity_cpus": affinity,
+            "by_threads": {str(k): round(samples / v[0], 1) for k, v in timed.items()},
             "sample": f"oracle/torch_ref.synth_path (reference ATen op sequence), batch {B} of "
                       f"config {args.config} (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
-                      f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {len(times)} runs, "
-                      f"{t:.3f} s each"}
+                      f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {reps} runs, "
+                      f"{t:.3f} s each at {best} threads (faster of {sorted(timed)} threads; host "
+                      f"os.cpu_count() = {host})"}
 
 
 def train_leg(args, inp, dev, reps=20):
@@ -403,24 +431,41 @@ def main():
     value = samples_per_step * args.steps / elapsed
     traffic = load_traffic(args.traffic)
 
-    # dominant kernel: fused oscillator (per-launch = B*F*bs samples of this rank)
+    # dominant kernel: the fused synthesis kernel (per launch = B*F*bs samples of this rank).  Its
+    # bound is VALU issue (it reads only frame-rate controls): achieved = issue slots per launch
+    # (PMC SQ_INSTS_VALU of this kernel, each v_sin_f32 counted at 4 slots) / launch duration.
     osc_ms = timer.mean_ms("synth_frames")
-    osc_bytes = 4 * (H + 2) * B * F * bs
-    osc_gbs = osc_bytes / (osc_ms * 1e-3) / 1e9
     n_sin = B * F * bs * H
-    roofline = {"bound": "hbm", "achieved": round(osc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(osc_gbs / HBM_PEAK_GBS, 4),
+    osc_slots = n_sin / 64 * OSC_SLOTS_PER_SINE
+    vc = load_traffic(args.valu_counts).get(f"config{args.config}", {})
+    if vc.get("SQ_INSTS_VALU"):
+        slots = vc["SQ_INSTS_VALU"] + (SIN_SLOTS - 1) * n_sin / 64
+        slots_src = (f"PMC SQ_INSTS_VALU {vc['SQ_INSTS_VALU']:.4g} wave-instructions per launch "
+                     f"({args.valu_counts.replace(ROOT + os.sep, '')}) + {SIN_SLOTS - 1} extra slots per "
+                     "v_sin_f32 wave-instruction")
+    else:
+        slots = osc_slots
+        slots_src = "oscillator model only (no PMC counts for this configuration)"
+    achieved = slots / (osc_ms * 1e-3)
+    osc_bytes = 4 * (H + 2) * B * F * bs
+    roofline = {"bound": "valu", "achieved": round(achieved / 1e12, 4), "peak": VALU_PEAK_SLOTS / 1e12,
+                "unit": "T issue slots/s (wave64 VALU: fp32 op 1 slot = 2 SIMD cycles, v_sin_f32 4 slots)",
+                "frac": round(achieved / VALU_PEAK_SLOTS, 4),
                 "traffic": traffic.get("synth_frame_kernel"),
                 "kernel": "synth_frame_kernel (oscillator bank + filtered noise + their controls, fused)",
-                "algorithmic_bytes_per_launch": osc_bytes, "avg_launch_ms": round(osc_ms, 4),
-                "convention": "SURVEY 8(d): 4*(H+2) B/sample op-boundary bytes credited to the fused "
-                              "kernel; it physically reads only frame-rate controls",
+                "avg_launch_ms": round(osc_ms, 4), "slots_per_launch": round(slots),
+                "slots_source": slots_src,
+                "oscillator_frac": round(osc_slots / (osc_ms * 1e-3) / VALU_PEAK_SLOTS, 4),
                 "sines_per_s": round(n_sin / (osc_ms * 1e-3), 1),
-                "valu_frac": round(n_sin * OSC_VALU_SLOTS / (osc_ms * 1e-3) / VALU_PEAK_LANE_OPS, 4),
-                "valu_note": "the fused kernel is VALU-bound: valu_frac = sines/s x 9 VALU issue slots "
-                             "per (sample, harmonic: 6 VALU ops + one hardware sine at ~3 slots) / "
-                             "(256 CU x 128 lanes x 2.4 GHz); the noise FIR and controls in the same "
-                             "launch are not counted"}
+                "peak_note": "256 CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 fp32 VALU op (issue rate "
+                             "at >=2 waves/SIMD measured by tools/issue_probe.hip, profiles/"
+                             "r02_issue_probe.log; v_sin_f32 issues every 8 cycles)"}
+    # SURVEY 8(d)'s effective-bandwidth convention (op-boundary bytes 4*(H+2) B/sample credited to
+    # the fused kernel): NOT a roofline fraction - the fused kernel never moves these bytes
+    op_boundary_effective = {"gbs": round(osc_bytes / (osc_ms * 1e-3) / 1e9, 1),
+                             "algorithmic_bytes_per_launch": osc_bytes,
+                             "note": "SURVEY 8(d) convention: op-boundary bytes / fused-kernel time; "
+                                     "exceeds HBM peak because fusion removed that traffic"}
 
     result = {
         "metric": "audio samples/sec (48 kHz, 100 harm, blk=512) at 1/2/4/8 GPU; % HBM roofline",
@@ -433,11 +478,38 @@ def main():
                                f"n_harmonic {H}, n_bands {NB}, sr {sr}, reverb {args.reverb_length} taps",
                    "global_batch": B * world, "seq_len": F * bs, "parallelism": f"batch-shard x{world}"},
         "roofline": roofline,
+        "op_boundary_effective": op_boundary_effective,
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
         "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region "
                           "(the VALU-bound synthesis kernel runs up to ~20% slower once the device "
                           "is hot; roofline.avg_launch_ms is from inside the timed region)",
     }
+
+    if syn.reverb is not None and not args.no_uncached_leg:
+        # the reference rebuilds the impulse and its transform on every Reverb.forward
+        # (modules.py:30-33); the module caches the spectrum between calls.  Same step with the
+        # cache off: build_impulse + partition spectra + the rest, every call.
+        syn.reverb.cache_spectrum = False
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        tu = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        tu = time.perf_counter() - tu
+        syn.reverb.cache_spectrum = True
+        syn.reverb.invalidate()
+        if dist:
+            tt = torch.tensor([tu], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tu = float(tt.item())
+        result["uncached_ir"] = {"value": round(samples_per_step * args.steps / tu, 1), "unit": "samples/s",
+                                 "ms_per_step": round(tu / args.steps * 1e3, 4),
+                                 "note": "step with the reverb IR and its partition spectra rebuilt every call "
+                                         "(Reverb.cache_spectrum = False), as the reference's Reverb.forward does"}
 
     if dist and not args.no_gather:
         from ddsp_pytorch_amd.shard import gather_audio
@@ -506,7 +578,7 @@ def main():
         result["roofline_op"] = {"bound": "hbm", "achieved": round(op_gbs, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(op_gbs / HBM_PEAK_GBS, 4),
                                  "traffic": traffic.get("harmonic_samples_kernel"),
-                                 "kernel": "phase_chunk_sums_kernel + harmonic_samples_kernel<true>",
+                                 "kernel": "phase_chunk_sums_kernel + harmonic_samples_tiled_kernel",
                                  "avg_launch_ms": round(op_ms, 4)}
 
     if rank == 0 and not args.no_train_leg:

@@ -34,6 +34,17 @@ class Reverb(nn.Module):
         self.register_buffer("t", t.reshape(1, -1, 1))
         self._spec_key = None
         self._spec = None
+        # The IR spectrum is cached between forwards (the reference rebuilds it every call,
+        # modules.py:30-33).  The cache key holds the parameters' storage and autograd version
+        # counters: optimizer steps and in-place ops on the parameters invalidate it, writes through
+        # ``p.data`` (EMA copies, clamping via .data) do not — call invalidate() after those, or set
+        # cache_spectrum = False to rebuild on every forward as the reference does.
+        self.cache_spectrum = True
+
+    def invalidate(self):
+        """Drop the cached IR spectrum (rebuilt on the next forward)."""
+        self._spec_key = None
+        self._spec = None
 
     def build_impulse(self):
         """modules.py:21-26 -> [1, length, 1]."""
@@ -42,7 +53,7 @@ class Reverb(nn.Module):
     def _spectrum(self, n_samples):
         key = (n_samples, self.noise.device, self.noise.data_ptr(), self.noise._version,
                self.decay._version, self.wet._version, self.decay.data_ptr(), self.wet.data_ptr())
-        if key != getattr(self, "_spec_key", None):
+        if key != getattr(self, "_spec_key", None) or not getattr(self, "cache_spectrum", True):
             with torch.no_grad():
                 self._spec = core.reverb_spectrum(self.build_impulse(), n_samples)
             self._spec_key = key

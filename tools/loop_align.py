@@ -52,18 +52,35 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0EE"):
         if nsin >= 8 and (best is None or len(body) < len(best[2])):
             best = (nsin, target, body)
     if best is None:
-        print(f"{so}: no sine loop in {kern}")
-        return
+        return None
     _, start, body = best
-    eight=[x for x in body if x[1]==8]
-    mis=[x for x in eight if x[0]%8!=0]
-    print(f"{so.split('/')[-1]} {kern}: loop @{start:#x} (mod 8 = {start%8}), {len(body)} instrs, {sum(x[1] for x in body)} B, 8-byte {len(eight)}, misaligned {len(mis)}")
+    eight = [x for x in body if x[1] == 8]
+    mis = [x for x in eight if x[0] % 8 != 0]
+    return {"kernel": kern, "start": start, "instrs": len(body), "bytes": sum(x[1] for x in body),
+            "eight_byte": len(eight), "odd_dword": len(mis),
+            "sines": sum(1 for x in body if x[2].startswith("v_sin_f32"))}
+
+
+# every shipped instantiation with a hardware-sine loop: fused forward (device noise / injected
+# noise, one sample per thread for few-frame launches), the harmonic-only fused backward
+SHIPPED = ("synth_frame_kernelILb1ELb0EE", "synth_frame_kernelILb0ELb0EE",
+           "synth_frame_kernelILb1ELb1EE", "synth_frame_kernelILb0ELb1EE",
+           "frame_backward_kernelILi2ELi2ELb1EE")
+
+
+def report(so, kern):
+    r = analyze(so, kern)
+    if r is None:
+        print(f"{so}: no sine loop in {kern}")
+    else:
+        print(f"{so.split('/')[-1]} {kern}: loop @{r['start']:#x} (mod 8 = {r['start'] % 8}), {r['instrs']} "
+              f"instrs, {r['bytes']} B, {r['sines']} sines, 8-byte {r['eight_byte']}, at odd dwords {r['odd_dword']}")
+    return r
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     libs = [a for a in sys.argv[1:] if a.endswith(".so")] or [
         os.path.join(root, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")]
-    kerns = [a for a in sys.argv[1:] if not a.endswith(".so")] or [
-        "synth_frame_kernelILb1ELb0EE", "frame_backward_kernelILi2ELi2ELb1EE"]
+    kerns = [a for a in sys.argv[1:] if not a.endswith(".so")] or list(SHIPPED)
     for so in libs:
         for k in kerns:
-            analyze(so, k)
+            report(so, k)
