@@ -66,6 +66,26 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
   acc = __builtin_elementwise_fma((v2f){a.y, a.y}, b_rot, acc);
 }
 
+#ifndef UPOLS_FWD_SWZ
+#define UPOLS_FWD_SWZ 1
+#endif
+#ifndef UPOLS_MAC_BLK
+#define UPOLS_MAC_BLK 25
+#endif
+
+// XCD-aware (block, pair) of a (nb, npairs) grid: workgroups round-robin over the 8 XCDs by linear
+// id, so XCD x gets ids x, x+8, ...; remapped, XCD x walks a contiguous run of the (pair, block)
+// sequence and consecutive blocks of a pair share its L2 (the overlap-save windows overlap by
+// half: block b re-reads the half that block b-1 loaded).  Bijective: the ids past the last full
+// round of 8 keep their identity mapping.
+__device__ __forceinline__ void swizzled_block(int nb, int npairs, int& b, int& pair) {
+  const int64_t total = (int64_t)nb * npairs, id = blockIdx.x + (int64_t)nb * blockIdx.y;
+  const int64_t per = total >> 3;
+  const int64_t g = (UPOLS_FWD_SWZ && id < (per << 3)) ? (id & 7) * per + (id >> 3) : id;
+  pair = (int)(g / nb);
+  b = (int)(g - (int64_t)pair * nb);
+}
+
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
   if (pairing) {
@@ -87,7 +107,9 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
                                                             int off, int zero_half, int reverse,
                                                             float2* __restrict__ X) {
   __shared__ float2 lds[kPad];
-  const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
+  const int j = threadIdx.x;
+  int b, pair;
+  swizzled_block(nb, (int)gridDim.y, b, pair);
   int ra, rb;
   pair_rows(pair, rows, pairing, ra, rb);
   const float* xa = x + (int64_t)ra * ld;
@@ -376,11 +398,13 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   int st = launch_status();
   if (st) return st;
   const int64_t h_stride = per_row_kernel ? upols_partitions(klen) * kN : 0;
-  // 16 output blocks per thread: each X row is re-read (Q+15)/16 times through L2
+  // UPOLS_MAC_BLK (25) output blocks per thread: each X row is re-read (Q+BLK-1)/BLK times through L2
+  // (A/B at config 2: 25 blocks 26.6 us vs 16 blocks 28.3 us, 8 and 32 no better)
   // (measured slower: an LDS-tiled variant that reads X once, 25%: lower occupancy, exposed
   // loads; every operand loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one
   // thread per (pair, bin) streaming all blocks with a register ring, 8%)
-  hipLaunchKernelGGL(upols_mac_kernel<16>, dim3(kN / kNT, (unsigned)((nb + 15) / 16), (unsigned)npairs),
+  constexpr int BLK = UPOLS_MAC_BLK;
+  hipLaunchKernelGGL(upols_mac_kernel<BLK>, dim3(kN / kNT, (unsigned)((nb + BLK - 1) / BLK), (unsigned)npairs),
                      dim3(kNT), 0, S(stream), X, reinterpret_cast<const float2*>(spectrum), h_stride,
                      (int)nb, (int)Q, Y);
   if ((st = launch_status())) return st;
