@@ -352,6 +352,69 @@ def decoder_leg(args, inp, dev, reps=10):
                      f"{args.reverb_length}), random init, batch {B} x {F} frames"}
 
 
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _max_over_ranks(seconds, dev, dist):
+    t = torch.tensor([seconds], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gathered_leg(step, global_batch, samples_per_step, steps, dev, dist):
+    """N>1 leg (SURVEY 8(e) "gathered to rank 0"): every rank synthesises its shard (``step()``
+    returns this rank's [b_r, T, 1] slice of a ``global_batch``-item batch, ragged shards allowed)
+    and the audio is gathered on rank 0 (torch.distributed.gather: RCCL over xGMI on MI355X, gloo
+    in the CPU tests).  Timed between barrier + device sync on both sides, max over ranks.
+    Returns (result dict, the last gathered batch on rank 0 / None elsewhere)."""
+    from ddsp_pytorch_amd.shard import gather_audio
+    _sync(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    g = None
+    for _ in range(steps):
+        g = gather_audio(step(), global_batch)
+    _sync(dev)
+    dist.barrier()
+    t = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    backend = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+    return ({"value": round(samples_per_step * steps / t, 1), "unit": "samples/s",
+             "collective": f"torch.distributed.gather ({backend})",
+             "ms_per_step": round(t / steps * 1e3, 4)}, g)
+
+
+def scatter_gather_leg(synth, held, global_batch, tails, samples_per_step, steps, chunks, dev, dist,
+                       reverb=None, warm=2):
+    """N>1 leg (SURVEY 8(e) root-held batch): rank 0 holds the frame-rate controls of all
+    ``global_batch`` items (``held``: full-batch tensors in the order ``synth`` takes them, None on
+    the other ranks; ``tails``: their per-item shapes), scatters them in ``chunks`` pieces, every
+    rank synthesises its shard and the audio is gathered back on rank 0, the collectives of one
+    chunk overlapping the synthesis of its neighbours (shard.synthesize_pipelined).  The reverb IR
+    is broadcast once first.  Returns (result dict, the last gathered batch on rank 0)."""
+    from ddsp_pytorch_amd.shard import broadcast_module, synthesize_pipelined
+    if reverb is not None:
+        broadcast_module(reverb)
+    pipe = lambda: synthesize_pipelined(synth, held, global_batch, tails, chunks=chunks, device=dev)
+    for _ in range(warm):
+        pipe()
+    _sync(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    g = None
+    for _ in range(steps):
+        g = pipe()
+    _sync(dev)
+    dist.barrier()
+    t = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    backend = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+    return ({"value": round(samples_per_step * steps / t, 1), "unit": "samples/s",
+             "ms_per_step": round(t / steps * 1e3, 4), "chunks": chunks,
+             "collective": f"torch.distributed scatter (controls) + gather (audio), {backend}, async per chunk"},
+            g)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -512,26 +575,11 @@ def main():
                                          "(Reverb.cache_spectrum = False), as the reference's Reverb.forward does"}
 
     if dist and not args.no_gather:
-        from ddsp_pytorch_amd.shard import gather_audio
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        for _ in range(args.steps):
-            g = gather_audio(step(), B * world)
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter() - tg
-        tt = torch.tensor([tg], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        result["gathered"] = {"value": round(samples_per_step * args.steps / float(tt.item()), 1),
-                              "unit": "samples/s", "collective": "torch.distributed.gather (RCCL)",
-                              "ms_per_step": round(float(tt.item()) / args.steps * 1e3, 4)}
+        r, g = gathered_leg(step, B * world, samples_per_step, args.steps, dev, dist)
+        result["gathered"] = r
         del g
         # root-held batch: controls scattered from rank 0 in chunks, audio gathered back,
         # scatter(i+1) || synth(i) || gather(i-1) (shard.synthesize_pipelined); IR broadcast once
-        from ddsp_pytorch_amd.shard import broadcast_module, synthesize_pipelined
-        if syn.reverb is not None:
-            broadcast_module(syn.reverb)
         keys = ["f0", "param", "mags"] + (["noise"] if args.noise == "inject" else [])
         tails = [tuple(inp[k].shape[1:]) for k in keys]
         held = None
@@ -539,23 +587,9 @@ def main():
             full = make_inputs(B * world, F, H, NB, bs, seed=0, device=dev,
                                with_noise=(args.noise == "inject"))
             held = [full[k] for k in keys]
-        pipe = lambda: synthesize_pipelined(syn, held, B * world, tails, chunks=args.chunks, device=dev)
-        for _ in range(2):
-            pipe()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tp = time.perf_counter()
-        for _ in range(args.steps):
-            g = pipe()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tp = time.perf_counter() - tp
-        tt = torch.tensor([tp], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        result["scatter_gather"] = {
-            "value": round(samples_per_step * args.steps / float(tt.item()), 1), "unit": "samples/s",
-            "ms_per_step": round(float(tt.item()) / args.steps * 1e3, 4), "chunks": args.chunks,
-            "collective": "torch.distributed scatter (controls) + gather (audio), RCCL, async per chunk"}
+        r, g = scatter_gather_leg(syn, held, B * world, tails, samples_per_step, args.steps, args.chunks,
+                                  dev, dist, reverb=syn.reverb)
+        result["scatter_gather"] = r
         del g, held
 
     if rank == 0 and not args.no_op_leg:

@@ -1,0 +1,113 @@
+"""bench.py's N>1 legs executed on CPU with gloo at world size 2, before any
+multi-GPU run: "gathered" (every rank synthesises its shard, audio gathered on rank 0) and
+"scatter_gather" (root-held controls scattered in chunks, audio gathered back, IR broadcast).
+
+The HIP kernels cannot run here, so the synth callable is the torch-CPU restatement of the
+reference path (oracle/torch_ref.py) for the small case, and a cheap deterministic map from
+controls to audio for the config-5-shaped case (400 frames, 128 harmonics, 65 bands, block 512),
+where the point is the collectives' shapes and the ragged shards, not the synthesis."""
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        import bench
+        from oracle import torch_ref as tr
+        from ddsp_pytorch_amd.modules import Reverb
+        from ddsp_pytorch_amd.shard import shard
+        from ddsp_pytorch_amd.synth import make_inputs
+        cpu = torch.device("cpu")
+
+        # --- small case through the reference algorithm, ragged shards (3 + 2 items) ---
+        batch, F, H, NB, bs = 5, 4, 16, 9, 64
+        inp = make_inputs(batch, F, H, NB, bs, seed=0)
+        torch.manual_seed(1)
+        noise = (torch.rand(300) * 2 - 1).unsqueeze(-1)
+        rv = tr.Reverb(noise, torch.tensor(5.0), torch.tensor(0.0), 300, 48000)
+        synth = lambda f0, p, m, n: tr.synth_path(f0, p, m, n, rv, bs, 48000)
+        local = {k: shard(v, rank, world) for k, v in inp.items()}
+        step = lambda: synth(local["f0"], local["param"], local["mags"], local["noise"])
+        sps = batch * F * bs
+        r1, g1 = bench.gathered_leg(step, batch, sps, 2, cpu, dist)
+        keys = ["f0", "param", "mags", "noise"]
+        tails = [tuple(inp[k].shape[1:]) for k in keys]
+        held = [inp[k] for k in keys] if rank == 0 else None
+        reverb = Reverb(300, 48000)
+        with torch.no_grad():  # rank 1's parameters differ until the leg broadcasts rank 0's
+            reverb.decay.fill_(5.0 + rank)
+        r2, g2 = bench.scatter_gather_leg(synth, held, batch, tails, sps, 2, 2, cpu, dist, reverb=reverb, warm=1)
+        res = {"r1": r1, "r2": r2, "decay": float(reverb.decay)}
+        if rank == 0:
+            full = synth(inp["f0"], inp["param"], inp["mags"], inp["noise"])
+            res["err1"] = float((g1 - full).abs().max())
+            res["err2"] = float((g2 - full).abs().max())
+            res["shape"] = tuple(g1.shape)
+
+        # --- config-5-shaped items (F=400, H=128, NB=65, bs=512), 4 items, 2 chunks, cheap synth ---
+        batch5, F5, H5, NB5, bs5 = 4, 400, 128, 65, 512
+        inp5 = make_inputs(batch5, F5, H5, NB5, bs5, seed=3, with_noise=False)
+        cheap = lambda f0, p, m: (f0 + p.sum(-1, keepdim=True) - m.mean(-1, keepdim=True)).repeat_interleave(bs5, 1)
+        keys5 = ["f0", "param", "mags"]
+        tails5 = [tuple(inp5[k].shape[1:]) for k in keys5]
+        held5 = [inp5[k] for k in keys5] if rank == 0 else None
+        r5, g5 = bench.scatter_gather_leg(cheap, held5, batch5, tails5, batch5 * F5 * bs5, 1, 2, cpu, dist, warm=0)
+        local5 = {k: shard(v, rank, world) for k, v in inp5.items()}
+        r6, g6 = bench.gathered_leg(lambda: cheap(local5["f0"], local5["param"], local5["mags"]), batch5,
+                                    batch5 * F5 * bs5, 1, cpu, dist)
+        if rank == 0:
+            full5 = cheap(inp5["f0"], inp5["param"], inp5["mags"])
+            res["err5"] = float((g5 - full5).abs().max())
+            res["err6"] = float((g6 - full5).abs().max())
+            res["shape5"] = tuple(g5.shape)
+            res["r5"] = r5
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_n_gt_1_legs_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0 = out[0]
+    assert r0["shape"] == (5, 4 * 64, 1)
+    # the gathered shards are the full-batch synthesis item for item; the chunked leg calls the synth on
+    # different item groupings, and MKL's batched FFT rounds a different batch size differently (fp32 ulps)
+    assert r0["err1"] == 0.0 and r0["err2"] < 1e-6, r0
+    assert r0["err5"] == 0.0 and r0["err6"] == 0.0 and r0["shape5"] == (4, 400 * 512, 1)
+    for rank in range(world):  # the IR parameters were broadcast from rank 0
+        assert out[rank]["decay"] == 5.0
+        for leg in ("r1", "r2"):
+            d = out[rank][leg]
+            assert d["unit"] == "samples/s" and d["value"] > 0 and d["ms_per_step"] > 0
+            assert "gloo" in d["collective"]
+    assert out[0]["r2"]["chunks"] == 2 and out[0]["r5"]["value"] > 0
