@@ -235,20 +235,101 @@ def test_decoder_golden(dd):
         assert e < PARITY_RMS, (key, e)
 
 
+def _reference_shaped_modules():
+    """Classes carrying exactly the reference's instance attributes (modules.py:7-128: the
+    constructors' fields, parameters and buffers) and none of this package's extras
+    (noise_mode, _spec_key, _spec, cache_spectrum) - what install() finds on real reference
+    instances.  Their methods are placeholders that install() replaces."""
+    import types
+    import torch.nn as nn
+
+    class Reverb(nn.Module):
+        def __init__(self, length, sample_rate, initial_wet=0, initial_decay=5):
+            super().__init__()
+            self.length, self.sample_rate = length, sample_rate
+            self.noise = nn.Parameter((torch.rand(length) * 2 - 1).unsqueeze(-1))
+            self.decay = nn.Parameter(torch.tensor(float(initial_decay)))
+            self.wet = nn.Parameter(torch.tensor(float(initial_wet)))
+            self.register_buffer("t", (torch.arange(length) / sample_rate).reshape(1, -1, 1))
+
+    class HarmonicSynth(nn.Module):
+        def __init__(self, block_size, sample_rate):
+            super().__init__()
+            self.block_size, self.sample_rate = block_size, sample_rate
+
+    class FilteredNoise(nn.Module):
+        def __init__(self, block_size, window_size, initial_bias=-5.0):
+            super().__init__()
+            self.block_size, self.window_size, self.initial_bias = block_size, window_size, initial_bias
+
+    for cls in (Reverb, HarmonicSynth, FilteredNoise):
+        for name in ("forward", "get_controls", "build_impulse", "draw_noise", "_spectrum"):
+            setattr(cls, name, lambda self, *a: None)
+    return types.SimpleNamespace(Reverb=Reverb, HarmonicSynth=HarmonicSynth, FilteredNoise=FilteredNoise)
+
+
 def test_install_into_reference_style_package(dd):
-    """install() rebinds late-bound functions; exercised on a package shaped like the reference."""
+    """install() into a package laid out like the reference (ddsp.<fn> late-bound functions, bound
+    to the oracle's restatements before install; synth module classes with only the reference's
+    instance attributes), then VALUES through the installed package against the oracle
+    (<= 1e-6 RMS): the six functions chained as HarmonicSynth.forward / FilteredNoise.forward
+    chain them (modules.py:69-80, 116-128), and the swapped module methods on reference-shaped
+    instances, the reverb included.  (The real reference package is checked in the development
+    container: tests/test_install_reference.py.)"""
     import types
     pkg = types.ModuleType("ddsp_like")
     for name in ("scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
                  "amp_to_impulse_response", "fft_convolve"):
         setattr(pkg, name, getattr(tr, name))
-    inst = dd.install(pkg, module_forwards=False)
+    pkg.models = types.SimpleNamespace(modules=_reference_shaped_modules())
+    B, F, H, NB, bs, sr = 2, 8, 16, 9, 64, 48000
+    rng = np.random.default_rng(0)
+    f0 = (50.0 * 20.0 ** rng.random((B, F, 1))).astype(np.float32)
+    raw_amp = rng.standard_normal((B, F, 1)).astype(np.float32)
+    raw_dist = rng.standard_normal((B, F, H)).astype(np.float32)
+    raw_mags = rng.standard_normal((B, F, NB)).astype(np.float32)
+    noise = (rng.random((B, F, bs)) * 2 - 1).astype(np.float32)
+    T = lambda x: torch.as_tensor(x)
+    # oracle (reference ATen sequence) on the CPU
+    amps_r, dist_r = tr.harmonic_controls(T(raw_amp), T(raw_dist), T(f0), sr)
+    harm_r = tr.harmonic_forward(amps_r, dist_r.clone(), T(f0), bs, sr)
+    mags_r = tr.scale_function(T(raw_mags) - 5.0)
+    noise_r = tr.noise_forward(mags_r, T(noise), bs)
+
+    inst = dd.install(pkg)
     try:
-        f0 = G(50.0 * 20.0 ** np.random.default_rng(0).random((1, 4, 1)))
-        a = torch.rand(1, 4, 8, device="cuda")
+        # the function level: ddsp.<fn> now runs the gfx950 kernels
         with torch.no_grad():
-            out = pkg.harmonic_synth(pkg.upsample(f0, 64), pkg.upsample(a, 64), 48000)
-        assert out.is_cuda and out.shape == (1, 256, 1)
+            amps = pkg.scale_function(G(raw_amp))
+            dist = pkg.remove_above_nyquist(pkg.scale_function(G(raw_dist)), G(f0), sr)
+            dist = dist / dist.sum(-1, keepdim=True)
+            harm = pkg.harmonic_synth(pkg.upsample(G(f0), bs), pkg.upsample(dist * amps, bs), sr)
+            ir = pkg.amp_to_impulse_response(pkg.scale_function(G(raw_mags) - 5.0), bs)
+            nz = pkg.fft_convolve(G(noise), ir).reshape(B, -1, 1)
+        assert rms(C(harm), harm_r.numpy()) < 1e-6
+        assert rms(C(nz), noise_r.numpy()) < 1e-6
+        # the module level: swapped methods on instances with only the reference's attributes
+        mods = pkg.models.modules
+        hs = mods.HarmonicSynth(bs, sr)
+        fn = mods.FilteredNoise(bs, NB)
+        torch.manual_seed(1)
+        rv = mods.Reverb(1000, sr).cuda()
+        with torch.no_grad():
+            ctrl = hs.get_controls(G(raw_amp), G(raw_dist), G(f0))
+            harm2 = hs(ctrl["amplitudes"], ctrl["harmonic_distribution"], ctrl["f0"])
+            torch.manual_seed(123)  # the reference's noise draw: torch.rand(B, F, bs) * 2 - 1
+            nz2 = fn(fn.get_controls(G(raw_mags))["magnitudes"])
+            wet = rv(harm2 + nz2)
+        torch.manual_seed(123)
+        noise_t = torch.rand(B, F, bs) * 2 - 1
+        noise_r2 = tr.noise_forward(mags_r, noise_t, bs)
+        rv_r = tr.Reverb(rv.noise.detach().cpu(), rv.decay.detach().cpu(), rv.wet.detach().cpu(), 1000, sr)
+        wet_r = rv_r(harm_r + noise_r2)
+        assert rms(C(harm2), harm_r.numpy()) < 1e-6
+        assert rms(C(nz2), noise_r2.numpy()) < 1e-6
+        # reverb: the partitioned FFT against one 2T-point FFT, as the other reverb tests
+        assert rms(C(wet), wet_r.numpy()) < 2e-6 * max(1.0, float(wet_r.pow(2).mean().sqrt()))
+        assert not hasattr(rv, "cache_spectrum") and not hasattr(fn, "noise_mode")
     finally:
         inst.uninstall()
     assert pkg.harmonic_synth is tr.harmonic_synth

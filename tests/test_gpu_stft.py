@@ -76,6 +76,9 @@ def test_spectral_loss_golden(dd):
     val = L.multiscale_spec_loss(dd.core.multiscale_fft(sig, scales, overlap), rs)
     assert relerr(val, g["loss"]) < 1e-5, (float(val), float(g["loss"]))
     val.backward()
+    # the golden gradient itself is 3.5e-4 from the fp64 gradient of the same loss (ill-conditioned
+    # log-term weights of the smallest bins); the 1e-5 comparison on the well-conditioned bins is
+    # test_spectral_loss_grad_well_conditioned_bins
     assert relerr(rec.grad, g["grad_rec"]) < 1e-3, relerr(rec.grad, g["grad_rec"])
 
 
@@ -134,3 +137,52 @@ def test_fused_spectral_loss_matches_unfused(dd):
     r2 = s2 + 0.05 * torch.randn(4, 102400, generator=gg)
     lc = tr.multiscale_spec_loss(tr.multiscale_fft(s2, scales, 0.75), tr.multiscale_fft(r2, scales, 0.75))
     assert relerr(L.spectral_loss(s2.cuda(), r2.cuda()), lc) < 1e-5
+
+
+def test_spectral_loss_grad_well_conditioned_bins(dd):
+    """Golden g7's gradient at 1e-5 on the bins where it is defined to that precision.
+
+    train.py's log-L1 term weights each bin by 1/(|Y| + 1e-7), so the loss gradient is dominated
+    by the few smallest magnitudes, whose fp32 transform round-off is of their own size: the
+    reference's own fp32 gradient (the golden) is 3.5e-4 (relative L2) from the same loss evaluated
+    in fp64, and no sign of an L1 term is a tie on g7 (tools/exp_loss_grad.py).  Masking the bins
+    with |X| or |Y| below 1 % of the spectrogram's RMS (0.14 % of all bins, mask taken from the
+    fp64 magnitudes) makes the reference's fp32 gradient agree with fp64 to 2.7e-6; on the
+    remaining bins the kernels' gradient must match the reference's at 1e-5.  The fused loss
+    (no mask input) is held to the reference's own accuracy against the fp64 gradient."""
+    from ddsp_pytorch_amd import loss as L
+    g = load_golden("g7_stft_loss")
+    scales, ov = [int(s) for s in g["scales"]], float(g["overlap"])
+    sig32, rec32 = torch.as_tensor(g["sig"]), torch.as_tensor(g["rec"])
+    ori64 = tr.multiscale_fft(sig32.double(), scales, ov)
+    my64 = tr.multiscale_fft(rec32.double(), scales, ov)
+    masks = []
+    for mx, my in zip(ori64, my64):
+        floor = 1e-2 * float(my.pow(2).mean().sqrt())
+        masks.append(((my > floor) & (mx > floor)).float())
+
+    def masked_loss(ori, rec_stft, log):
+        lo = 0
+        for m, mx, my in zip(masks, ori, rec_stft):
+            m = m.to(my)
+            lo = lo + (m * (mx - my).abs()).mean() + (m * (log(mx) - log(my)).abs()).mean()
+        return lo
+
+    def oracle_grad(dtype):
+        rc = rec32.to(dtype).clone().requires_grad_(True)
+        masked_loss(tr.multiscale_fft(sig32.to(dtype), scales, ov), tr.multiscale_fft(rc, scales, ov),
+                    tr.safe_log).backward()
+        return rc.grad
+    ref32, ref64 = oracle_grad(torch.float32), oracle_grad(torch.float64)
+    assert relerr(ref32, ref64) < 5e-6  # the reference's fp32 gradient is well conditioned here
+    rg = rec32.cuda().requires_grad_(True)
+    masked_loss(dd.core.multiscale_fft(sig32.cuda(), scales, ov), dd.core.multiscale_fft(rg, scales, ov),
+                dd.core.safe_log).backward()
+    assert relerr(rg.grad, ref32) < 1e-5, relerr(rg.grad, ref32)
+    # unmasked: the fused kernel's gradient is as close to the fp64 gradient as the reference's own
+    rc64 = rec32.double().clone().requires_grad_(True)
+    tr.multiscale_spec_loss(tr.multiscale_fft(sig32.double(), scales, ov), tr.multiscale_fft(rc64, scales, ov)).backward()
+    golden_err = relerr(g["grad_rec"], rc64.grad)
+    rf = rec32.cuda().requires_grad_(True)
+    L.spectral_loss(sig32.cuda(), rf, scales, ov).backward()
+    assert relerr(rf.grad, rc64.grad) < 2.0 * golden_err, (relerr(rf.grad, rc64.grad), golden_err)
