@@ -140,5 +140,15 @@ def stream_of(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+class _TensorPtr(ctypes.c_void_p):
+    """A device pointer that keeps its tensor alive: callers write ``ptr(_c(x))``, and the contiguous
+    temporary must not return its memory to torch's caching allocator (which could hand it to the
+    next temporary) before the launch that reads it has been enqueued."""
+
+
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    if t is None:
+        return ctypes.c_void_p(0)
+    p = _TensorPtr(t.data_ptr())
+    p._tensor = t
+    return p

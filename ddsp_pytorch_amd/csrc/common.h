@@ -190,6 +190,29 @@ __device__ __forceinline__ void block_sum_double2(double& a, double& b, double* 
   }
 }
 
+// Sums of two doubles over the waves [w0, w0 + nw) of the workgroup (a thread group of whole
+// waves); every wave of the workgroup must call it (one barrier).  Result valid in the group.
+__device__ __forceinline__ void group_sum_double2(double& a, double& b, double* scratch /*>=2*waves*/, int w0,
+                                                  int nw) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64);
+    b += __shfl_down(b, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    scratch[2 * wid] = a;
+    scratch[2 * wid + 1] = b;
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  for (int i = w0; i < w0 + nw; ++i) {
+    a += scratch[2 * i];
+    b += scratch[2 * i + 1];
+  }
+}
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;

@@ -12,13 +12,17 @@ namespace ddsp {
 
 // cos(2*pi*q/n) table, q in [0, n): fp64-evaluated, rounded once — read from the FFT
 // twiddle table (same values) when n divides 4096, else computed in fp64.
-static __device__ __forceinline__ void fill_cos_table(float* ct, int n) {
+// (tid, nt): this thread's index in, and the size of, the thread group filling the table.
+static __device__ __forceinline__ void fill_cos_table(float* ct, int n, int tid, int nt) {
   if (4096 % n == 0) {
     const int stride = 4096 / n;
-    for (int q = threadIdx.x; q < n; q += blockDim.x) ct[q] = kTwiddle4096[2 * q * stride];
+    for (int q = tid; q < n; q += nt) ct[q] = kTwiddle4096[2 * q * stride];
   } else {
-    for (int q = threadIdx.x; q < n; q += blockDim.x) ct[q] = (float)cospi(2.0 * (double)q / (double)n);
+    for (int q = tid; q < n; q += nt) ct[q] = (float)cospi(2.0 * (double)q / (double)n);
   }
+}
+static __device__ __forceinline__ void fill_cos_table(float* ct, int n) {
+  fill_cos_table(ct, n, threadIdx.x, blockDim.x);
 }
 
 // irfft of NB real magnitudes (imaginary parts zero) at tap m: n = 2(NB-1),

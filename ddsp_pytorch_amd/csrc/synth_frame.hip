@@ -24,15 +24,19 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // SPLIT (few-frame launches, e.g. the realtime stream's 4 frames per call): the workgroup has
 // G times the threads of one 4-samples-per-thread frame and the oscillator bank runs one sample
 // per thread, so one frame's latency is spread over G times the waves.
-template <bool RNG, bool SPLIT>
-__global__ void __launch_bounds__(256) synth_frame_kernel(
+//
+// frame_synth: one frame (f, b) by a thread group of NT threads (tid in [0, NT), whole waves starting
+// at wave w0 of the workgroup) in the LDS region smem4; every wave of the workgroup calls it (its
+// barriers are workgroup barriers).  On return (true: the thread's samples j0..j0+3 are in the
+// frame) acc = harmonic, nz = filtered noise.
+// PAD: one s_nop ahead of the sine loop (code placement, see phase 5)
+template <bool RNG, bool SPLIT, bool PAD>
+__device__ __forceinline__ bool frame_synth(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
-    const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
-    float* __restrict__ noise_out, int F, int H,
-    int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
-  extern __shared__ float4 smem4[];
-  __shared__ double red[32];
+    const uint64_t* __restrict__ counter, int F, int H, int NB, int bs, float sr, int lo_end, int tail_start,
+    int pad, int f, int b, int tid, int NT, float4* smem4, double* red, int w0, float (&acc)[4],
+    float (&nz)[4], int& j0_out) {
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
   float2* coef = reinterpret_cast<float2*>(smem4);       // [H4] (k+1, amplitude)
@@ -44,7 +48,6 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   float* xbuf = tail + ((half + 3) & ~3);                 // [pad zeros | bs samples]
   float* x = xbuf + pad;
 
-  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, NT = blockDim.x;
   const int64_t frame = (int64_t)b * F + f;
   const float* f0b = f0 + (int64_t)b * F;
   const float* prow = param + frame * (H + 1);
@@ -60,7 +63,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
     part_d += (double)v;
   }
   for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * NB + k] + bias);  // modules.py:113
-  fill_cos_table(ct, n);
+  fill_cos_table(ct, n, tid, NT);
   for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
   const int quads = bs >> 2;
   if (RNG && counter) {  // graph-replayed streams: the Philox offset advances in device memory
@@ -79,7 +82,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
     }
     *reinterpret_cast<float4*>(x + 4 * t) = v;
   }
-  block_sum_double2(part_s, part_d, red);  // includes the barrier that publishes phase 1
+  group_sum_double2(part_s, part_d, red, w0, NT >> 6);  // includes the barrier that publishes phase 1
   const double S = part_s;                 // exact fp64 prefix over earlier frames
   const float norm = (float)part_d;        // dist.sum(-1)
   const float a = scale_fn(prow[0]);
@@ -121,6 +124,9 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   __syncthreads();
 
   // ---- phase 4: noise tail (taps past bs - n/2 reach only the last n/2 outputs) ----
+#ifdef DDSP_PROBE_NO_TAIL
+  if (false)
+#endif
   for (int l = tid; l < bs - tail_start; l += NT) {
     const int j = tail_start + l;
     float c = 0.0f;
@@ -132,7 +138,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   const int j0 = 4 * tid;
   const bool active = j0 < bs;
   const double dinc = (double)phase_inc(pitch0, sr);
-  float acc[4];
+  j0_out = j0;
   if (!SPLIT) {
     float w[4];
     bool fast = true;
@@ -143,10 +149,16 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
       fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
     }
     // loop placement: the sine loop runs ~10% faster when its 8-byte instructions sit at odd dword
-    // addresses (tools/loop_align.py); the injected-noise instantiation needs one
-    // dword of padding ahead of it to get there
-    if constexpr (!RNG) asm volatile("s_nop 0");
+    // addresses (tools/loop_align.py, pinned by tests/test_loop_align.py); PAD puts
+    // one dword of padding after an 8-byte alignment point ahead of it where an instantiation needs
+    // it (the alignment makes the placement independent of the code laid out before the kernel)
+    if constexpr (PAD) asm volatile(".p2align 3\n s_nop 0");
+    else asm volatile(".p2align 3");
+#ifdef DDSP_PROBE_NO_OSC
+    if (false) {
+#else
     if (active) {
+#endif
       if (fast) {
 #pragma unroll 4
         for (int k = 0; k < H4; ++k) {
@@ -197,15 +209,40 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
       acc[3] = h4.w;
     }
   }
-  if (!active) return;
+  if (!active) return false;
 
-  // ---- phase 6: filtered noise for the same samples, sum, store ----
+  // ---- phase 6: filtered noise for the same samples ----
+#ifdef DDSP_PROBE_NO_FIR
+  float4 y = make_float4(x[j0], x[j0 + 1], x[j0 + 2], x[j0 + 3]);
+#else
   float4 y = fir4(h, x, j0, lo_end, bs, bs);  // taps [0, lo_end); the wrapped taps are in tail[]
-  float nz[4] = {y.x, y.y, y.z, y.w};
+#endif
+  nz[0] = y.x;
+  nz[1] = y.y;
+  nz[2] = y.z;
+  nz[3] = y.w;
 #pragma unroll
   for (int s = 0; s < 4; ++s)
     if (j0 + s >= tail_start) nz[s] += tail[j0 + s - tail_start];
-  const int64_t o = frame * bs + j0;
+  return true;
+}
+
+template <bool RNG, bool SPLIT>
+__global__ void __launch_bounds__(256) synth_frame_kernel(
+    const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
+    float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
+    const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
+    float* __restrict__ noise_out, int F, int H,
+    int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
+  extern __shared__ float4 smem4[];
+  __shared__ double red[32];
+  float acc[4], nz[4];
+  int j0;
+  if (!frame_synth<RNG, SPLIT, SPLIT>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, F, H, NB, bs, sr, lo_end,
+                               tail_start, pad, blockIdx.x, blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc,
+                               nz, j0))
+    return;
+  const int64_t o = ((int64_t)blockIdx.y * F + blockIdx.x) * bs + j0;
   if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
   if (noise_out) *reinterpret_cast<float4*>(noise_out + o) = make_float4(nz[0], nz[1], nz[2], nz[3]);
   *reinterpret_cast<float4*>(out + o) =

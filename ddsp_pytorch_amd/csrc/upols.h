@@ -1,5 +1,6 @@
 // Uniformly partitioned overlap-save convolution (upols.hip): internal API of the library.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -21,6 +22,10 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
 int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
                 bool per_row_kernel, float* y, void* ws, size_t ws_bytes, void* stream,
                 bool reverse = false);
+// upols_apply after its forward transform: Z = the input block spectra FFT([x_b, 0]) of the packed
+// rows ([npairs][nb][kN], e.g. written by the fused synthesis kernel), Y = workspace of the same size.
+int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
+                        bool per_row_kernel, float* y, float2* Y, void* stream, bool reverse = false);
 // bytes of the input spectra X that upols_apply leaves at the start of its workspace (pairing)
 size_t upols_spectra_bytes(int64_t rows, int64_t n);
 // Backward of upols_apply with a kernel shared by all rows (pairing): dx[rows, n] (nullable) and

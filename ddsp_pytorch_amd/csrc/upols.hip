@@ -1,4 +1,4 @@
-// Uniformly partitioned overlap-save (UPOLS) FFT convolution for gfx950.
+// Uniformly partitioned FFT convolution (UPOLS) for gfx950.
 //
 // Replaces the reference's one-shot 2T-point FFT convolution (ddsp/core.py:169-176, used by
 // Reverb.forward, ddsp/models/modules.py:28-35) for long signals and kernels.  Only the first
@@ -10,13 +10,19 @@
 //   two real rows sharing one kernel are packed as z = x_a + i*x_b: the kernel is real, so
 //   z (*) h = (x_a (*) h) + i (x_b (*) h) — one complex FFT serves two rows with no
 //   Hermitian post-processing;
-//   kernel partitions h_p = h[pP, (p+1)P) -> H_p = FFT_N([h_p, 0]) / N   (computed once);
-//   forward:  X_b = FFT_N(z[(b-1)P, (b+1)P))                 (upols_forward_kernel)
-//   MAC:      Y_b = sum_p X_{b-p} H_p   per frequency bin     (upols_mac_kernel)
-//   inverse:  y[bP, (b+1)P) = last P points of IFFT_N(Y_b)    (upols_inverse_kernel)
+//   the overlap sits on the KERNEL side: the input blocks are zero-padded, the kernel windows
+//   overlap by half (q = 0..Q, Q = ceil(L/P), h_{-1} = h_Q = 0):
+//   kernel:   G_q = FFT_N([h_{q-1}, h_q]) / N                   (computed once per IR)
+//   forward:  Z_b = FFT_N([x_b, 0])                             (upols_forward_kernel)
+//   MAC:      Y_b = sum_{q=0..Q} Z_{b-q} G_q   per frequency bin (upols_mac_kernel)
+//   inverse:  y[bP, (b+1)P) = last P points of IFFT_N(Y_b)      (upols_inverse_kernel)
+//   (circular convolution of [x_{b-q}, 0] with [h_{q-1}, h_q]: its second half holds exactly the
+//   terms h[tau] x[bP + n - tau] with tau in ((q-1)P + n, qP + n], so the Q+1 terms cover every
+//   tau once.)  Against the input-overlap form (X_b = FFT([x_{b-1}, x_b]) = Z_{b-1} + (-1)^f Z_b,
+//   Q kernel spectra) each input sample is read once instead of twice, for one more MAC term.
 //
-// HBM traffic per real output sample: x read twice (overlap, 8 B), X write/read (16 B),
-// Y write/read (16 B), y write (4 B).
+// HBM traffic per real output sample: x read (4 B), Z write/read (16 B), Y write/read (16 B),
+// y write (4 B).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,25 +72,9 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
   acc = __builtin_elementwise_fma((v2f){a.y, a.y}, b_rot, acc);
 }
 
-#ifndef UPOLS_FWD_SWZ
-#define UPOLS_FWD_SWZ 1
-#endif
 #ifndef UPOLS_MAC_BLK
 #define UPOLS_MAC_BLK 25
 #endif
-
-// XCD-aware (block, pair) of a (nb, npairs) grid: workgroups round-robin over the 8 XCDs by linear
-// id, so XCD x gets ids x, x+8, ...; remapped, XCD x walks a contiguous run of the (pair, block)
-// sequence and consecutive blocks of a pair share its L2 (the overlap-save windows overlap by
-// half: block b re-reads the half that block b-1 loaded).  Bijective: the ids past the last full
-// round of 8 keep their identity mapping.
-__device__ __forceinline__ void swizzled_block(int nb, int npairs, int& b, int& pair) {
-  const int64_t total = (int64_t)nb * npairs, id = blockIdx.x + (int64_t)nb * blockIdx.y;
-  const int64_t per = total >> 3;
-  const int64_t g = (UPOLS_FWD_SWZ && id < (per << 3)) ? (id & 7) * per + (id >> 3) : id;
-  pair = (int)(g / nb);
-  b = (int)(g - (int64_t)pair * nb);
-}
 
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
@@ -97,19 +87,17 @@ __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& 
   }
 }
 
-// X[pair][b][:] = FFT(z[(b+off)P, (b+off+2)P)); grid (nb, npairs).
-//   off = -1: the overlap-save input windows; with zero_half = 1 the first half is zeroed:
-//   FFT([0, z_b]), the adjoint of the inverse transform's "keep the second half" (backward);
-//   zero_half = 2 zeroes the second half.  reverse: z read time-reversed (z'[s] = z[T-1-s],
-//   the transposed convolution of the input gradient).
+// X[pair][b][:] = FFT(z[(b+off)P, (b+off+2)P)) with one half zeroed; grid (nb, npairs).
+//   off = 0, zero_half = 2: Z_b = FFT([z_b, 0]), the zero-padded input blocks (forward);
+//   off = -1, zero_half = 1: FFT([0, z_b]), the adjoint of the inverse transform's "keep the
+//   second half" (backward).  reverse: z read time-reversed (z'[s] = z[T-1-s], the transposed
+//   convolution of the input gradient).
 __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
                                                             int64_t T, int rows, int pairing, int nb,
                                                             int off, int zero_half, int reverse,
                                                             float2* __restrict__ X) {
   __shared__ float2 lds[kPad];
-  const int j = threadIdx.x;
-  int b, pair;
-  swizzled_block(nb, (int)gridDim.y, b, pair);
+  const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
   int ra, rb;
   pair_rows(pair, rows, pairing, ra, rb);
   const float* xa = x + (int64_t)ra * ld;
@@ -129,28 +117,29 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
 }
 
-// H[row][p][:] = FFT([h[row][pP, pP+P) (within klen), 0]) / N; grid (Q, krows)
+// G[row][q][:] = FFT(h[row][(q-1)P, (q+1)P) (zero outside [0, klen))) / N, q = 0..Q;
+// grid (Q + 1, krows)
 __global__ void __launch_bounds__(kNT) upols_kernel_spectrum_kernel(const float* __restrict__ h,
-                                                                    int64_t ld, int64_t klen, int Q,
+                                                                    int64_t ld, int64_t klen, int QG,
                                                                     float2* __restrict__ Hs) {
   __shared__ float2 lds[kPad];
-  const int p = blockIdx.x, row = blockIdx.y, j = threadIdx.x;
+  const int q = blockIdx.x, row = blockIdx.y, j = threadIdx.x;
   const float* hr = h + (int64_t)row * ld;
   const float inv_n = 1.0f / (float)kN;
   float2 v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int n = j + 256 * r;
-    const int64_t s = (int64_t)p * kP + n;
-    v[r] = make_float2((n < kP && s < klen) ? hr[s] * inv_n : 0.0f, 0.0f);
+    const int64_t s = (int64_t)(q - 1) * kP + j + 256 * r;
+    v[r] = make_float2((s >= 0 && s < klen) ? hr[s] * inv_n : 0.0f, 0.0f);
   }
   fft4096<false>(v, lds);
-  float2* out = Hs + ((int64_t)row * Q + p) * kN;
+  float2* out = Hs + ((int64_t)row * QG + q) * kN;
 #pragma unroll
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
 }
 
-// Y[pair][b][f] = sum_p X[pair][b-p][f] * H[p][f]; each thread one bin, BLK consecutive blocks
+// Y[pair][b][f] = sum_q Z[pair][b-q][f] * G[q][f] (Q here = the number of kernel spectra, Q+1 of
+// the header); each thread one bin, BLK consecutive blocks
 // with a sliding window of X in registers.  grid (N/256, ceil(nb/BLK), npairs)
 // (Measured: a register double-buffered prefetch of the next partitions ran 5-10% slower — the
 // extra registers cost more occupancy than the hidden latency bought.)
@@ -224,20 +213,20 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
 // Backward of the partitioned convolution (Reverb.forward, modules.py:28-35), the adjoint of
 // each forward step (F = unnormalised FFT, its adjoint the unnormalised inverse):
 //   y_b = second half of F^-1(Y_b)           ->  dY_b = GZ_b = F([0, g_b])
-//   Y_b = sum_p X_{b-p} H_p                   ->  dX_j = sum_p conj(H_p) GZ_{j+p}   (upols_mac_adj_kernel)
-//                                                 dH_p = sum_b conj(X_{b-p}) GZ_b  (upols_corr_kernel)
-//   X_b = F([x_{b-1}, x_b])                   ->  dx_b = second half of F^-1(dX_b + (-1)^f dX_{b+1})
-//                                                 (the first half of F^-1(Z) is the second half of
-//                                                 F^-1((-1)^f Z)), so the forward's inverse kernel applies
-//   H_p = F([h_p, 0]) / N                     ->  dh_p = Re(first half of F^-1(dH_p)) / N
-// For a packed pair (z = x_a + i x_b, g likewise) the real part of F^-1(conj(X) GZ) is corr_a + corr_b:
-// the packed spectra are used as they are.  GZ is shared by both gradients, and X is the forward's.
+//   Y_b = sum_q Z_{b-q} G_q                   ->  dZ_k = sum_q conj(G_q) GZ_{k+q}   (upols_mac_adj_kernel)
+//                                                 dG_q = sum_b conj(Z_{b-q}) GZ_b  (upols_corr_kernel)
+//   Z_b = F([x_b, 0])                         ->  dx_b = first half of F^-1(dZ_b) = second half of
+//                                                 F^-1((-1)^f dZ_b), so the forward's inverse kernel applies
+//   G_q = F([h_{q-1}, h_q]) / N               ->  dh_p = Re(first half of F^-1(dG_{p+1}) + second half of
+//                                                 F^-1(dG_p)) / N = Re(second half of F^-1(dG_p + (-1)^f dG_{p+1})) / N
+// For a packed pair (z = x_a + i x_b, g likewise) the real part of F^-1(conj(Z) GZ) is corr_a + corr_b:
+// the packed spectra are used as they are.  GZ is shared by both gradients, and Z is the forward's.
 
-// dH_p[f] = sum_{pair in group} sum_j conj(X[pair][j][f]) * G[pair][j+p][f]: PC consecutive
-// partitions per thread with a sliding register window of conj(X).  A workgroup is 64 bins x
+// dG_q[f] = sum_{pair in group} sum_j conj(Z[pair][j][f]) * G[pair][j+q][f]: PC consecutive
+// lags per thread with a sliding register window of conj(Z).  A workgroup is 64 bins x
 // kCorrSlices waves; the waves take interleaved pairs of the group (pair = grp * S + s, stepping
 // by groups * S) and are summed through LDS, so the grid has (N/64) * ceil(Q/PC) * groups
-// workgroups and only `groups` partial spectra per partition reach HBM.
+// workgroups and only `groups` partial spectra per lag reach HBM.
 constexpr int kCorrSlices = 4;
 template <int PC>
 __global__ void __launch_bounds__(64 * kCorrSlices) upols_corr_kernel(const float2* __restrict__ Xz,
@@ -286,8 +275,8 @@ __global__ void __launch_bounds__(64 * kCorrSlices) upols_corr_kernel(const floa
   }
 }
 
-// T_j = sum_p conj(H_p) GZ_{j+p} for BLK+1 consecutive j, then V_j = T_j + (-1)^f T_{j+1} for the
-// BLK outputs (the inverse kernel's second half of F^-1(V_j) is dx_j).  grid (N/256, ceil(nb/BLK), npairs)
+// V_j = (-1)^f sum_q conj(G_q) GZ_{j+q} for BLK consecutive j (the inverse kernel's second half of
+// F^-1(V_j) is dx_j).  grid (N/256, ceil(nb/BLK), npairs)
 template <int BLK>
 __global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __restrict__ G,
                                                             const float2* __restrict__ Hs, int nb, int Q,
@@ -298,57 +287,61 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __rest
   const float2* Gp = G + (int64_t)pair * nb * kN + f;
   const float2* Hp = Hs + f;
   const float2 zero = make_float2(0.f, 0.f);
-  float2 win[BLK + 1];
-  v2f acc[BLK + 1];
+  float2 win[BLK];
+  v2f acc[BLK];
 #pragma unroll
-  for (int d = 0; d <= BLK; ++d) {
+  for (int d = 0; d < BLK; ++d) {
     acc[d] = (v2f){0.f, 0.f};
     const float2 gv = Gp[(int64_t)min(j0 + d, nb - 1) * kN];
-    win[d] = j0 + d < nb ? gv : zero;  // win[d] = GZ_{j0+d+p}
+    win[d] = j0 + d < nb ? gv : zero;  // win[d] = GZ_{j0+d+q}
   }
-  const int pmax = min(Q, nb - j0);
+  const int qmax = min(Q, nb - j0);
 #pragma unroll 4
-  for (int p = 0; p < pmax; ++p) {
-    const float2 h = Hp[(int64_t)p * kN];
+  for (int q = 0; q < qmax; ++q) {
+    const float2 h = Hp[(int64_t)q * kN];
     const v2f hc = {h.x, -h.y}, hcr = {h.y, h.x};  // conj(h) and its rotation
 #pragma unroll
-    for (int d = 0; d <= BLK; ++d) cmac(acc[d], win[d], hc, hcr);
+    for (int d = 0; d < BLK; ++d) cmac(acc[d], win[d], hc, hcr);
 #pragma unroll
-    for (int d = 0; d < BLK; ++d) win[d] = win[d + 1];
-    const int kn = j0 + BLK + p + 1;
+    for (int d = 0; d < BLK - 1; ++d) win[d] = win[d + 1];
+    const int kn = j0 + BLK + q;
     const float2 gv = Gp[(int64_t)min(kn, nb - 1) * kN];
-    win[BLK] = kn < nb ? gv : zero;
+    win[BLK - 1] = kn < nb ? gv : zero;
   }
   const float sgn = (f & 1) ? -1.0f : 1.0f;
   float2* Vp = V + (int64_t)pair * nb * kN + f;
 #pragma unroll
   for (int d = 0; d < BLK; ++d)
-    if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(fmaf(sgn, acc[d + 1].x, acc[d].x),
-                                                               fmaf(sgn, acc[d + 1].y, acc[d].y));
+    if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(sgn * acc[d].x, sgn * acc[d].y);
 }
 
-// dimp[pP + n] = Re(IFFT(sum_groups part[grp][p])) [n] / N for n < P, pP + n < klen; grid (Q)
+// dimp[pP + n] = Re(IFFT(sum_groups part[grp][p] + (-1)^f part[grp][p+1])) [P + n] / N for n < P,
+// pP + n < klen (part holds Q + 1 lags; lag Q + 1 is zero); grid (Q)
 __global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __restrict__ part, int groups,
-                                                                int Q, int64_t klen, float* __restrict__ dimp) {
+                                                                int QG, int64_t klen, float* __restrict__ dimp) {
   __shared__ float2 lds[kPad];
   const int p = blockIdx.x, j = threadIdx.x;
   float2 v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = make_float2(0.f, 0.f);
   for (int g = 0; g < groups; ++g) {
-    const float2* in = part + ((int64_t)g * Q + p) * kN;
+    const float2* in = part + ((int64_t)g * QG + p) * kN;
+    const bool next = p + 1 < QG;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float2 w = in[j + 256 * r];
-      v[r].x += w.x;
-      v[r].y += w.y;
+      const int f = j + 256 * r;
+      const float2 w = in[f];
+      const float2 w1 = next ? in[kN + f] : make_float2(0.f, 0.f);
+      const float sg = (f & 1) ? -1.0f : 1.0f;
+      v[r].x += w.x + sg * w1.x;
+      v[r].y += w.y + sg * w1.y;
     }
   }
   fft4096<true>(v, lds);
   const float inv_n = 1.0f / (float)kN;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int64_t s = (int64_t)p * kP + j + 256 * r;
+  for (int r = 8; r < 16; ++r) {
+    const int64_t s = (int64_t)p * kP + j + 256 * r - kP;
     if (s < klen) dimp[s] = v[r].x * inv_n;
   }
 }
@@ -365,8 +358,11 @@ static int64_t corr_groups(int64_t npairs) {
 int64_t upols_partitions(int64_t klen) { return (std::max<int64_t>(klen, 1) + kP - 1) / kP; }
 int64_t upols_blocks(int64_t n) { return (n + kP - 1) / kP; }
 
+// kernel spectra per row: G_0 .. G_Q
+static int64_t upols_kernel_windows(int64_t klen) { return upols_partitions(klen) + 1; }
+
 size_t upols_spectrum_floats(int64_t krows, int64_t klen) {
-  return (size_t)krows * (size_t)upols_partitions(klen) * kN * 2;
+  return (size_t)krows * (size_t)upols_kernel_windows(klen) * kN * 2;
 }
 
 size_t upols_workspace_bytes(int64_t rows, int64_t n, bool pairing) {
@@ -376,10 +372,34 @@ size_t upols_workspace_bytes(int64_t rows, int64_t n, bool pairing) {
 
 int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, float* spectrum,
                    void* stream) {
-  const int64_t Q = upols_partitions(klen);
-  if (Q > 65535 || krows > 65535) return DDSP_HIP_EINVAL;
-  hipLaunchKernelGGL(upols_kernel_spectrum_kernel, dim3((unsigned)Q, (unsigned)krows), dim3(kNT), 0,
-                     S(stream), h, ld, klen, (int)Q, reinterpret_cast<float2*>(spectrum));
+  const int64_t QG = upols_kernel_windows(klen);
+  if (QG > 65535 || krows > 65535) return DDSP_HIP_EINVAL;
+  hipLaunchKernelGGL(upols_kernel_spectrum_kernel, dim3((unsigned)QG, (unsigned)krows), dim3(kNT), 0,
+                     S(stream), h, ld, klen, (int)QG, reinterpret_cast<float2*>(spectrum));
+  return launch_status();
+}
+
+int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
+                        bool per_row_kernel, float* y, float2* Y, void* stream, bool reverse) {
+  const bool pairing = !per_row_kernel;
+  const int64_t npairs = pairing ? (rows + 1) / 2 : rows;
+  const int64_t nb = upols_blocks(n);
+  const int64_t Q = upols_kernel_windows(std::min(klen, n));
+  const int64_t h_stride = per_row_kernel ? upols_kernel_windows(klen) * kN : 0;
+  constexpr int BLK = UPOLS_MAC_BLK;
+  if (nb > INT32_MAX || npairs > 65535 || (nb + BLK - 1) / BLK > 65535) return DDSP_HIP_EINVAL;
+  // UPOLS_MAC_BLK (25) output blocks per thread: each Z row is re-read (Q+BLK-1)/BLK times through L2
+  // (A/B at config 2: 25 blocks 26.6 us vs 16 blocks 28.3 us, 8 and 32 no better; measured slower:
+  // an LDS-tiled variant that reads Z once, 25%: lower occupancy, exposed loads; every operand
+  // loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one thread per (pair, bin)
+  // streaming all blocks with a register ring, 8%)
+  hipLaunchKernelGGL(upols_mac_kernel<BLK>, dim3(kN / kNT, (unsigned)((nb + BLK - 1) / BLK), (unsigned)npairs),
+                     dim3(kNT), 0, S(stream), Z, reinterpret_cast<const float2*>(spectrum), h_stride,
+                     (int)nb, (int)Q, Y);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
+                     Y, (int)nb, n, (int)rows, (int)pairing, (int)reverse, y, n);
   return launch_status();
 }
 
@@ -388,29 +408,16 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   const bool pairing = !per_row_kernel;
   const int64_t npairs = pairing ? (rows + 1) / 2 : rows;
   const int64_t nb = upols_blocks(n);
-  const int64_t Q = upols_partitions(std::min(klen, n));
   if (!ws || ws_bytes < upols_workspace_bytes(rows, n, pairing)) return DDSP_HIP_EWORKSPACE;
-  if (nb > INT32_MAX || npairs > 65535 || (nb + 15) / 16 > 65535) return DDSP_HIP_EINVAL;
+  if (nb > INT32_MAX || npairs > 65535) return DDSP_HIP_EINVAL;
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
+  // Z_b = FFT([x_b, 0])
   hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     x, n, n, (int)rows, (int)pairing, (int)nb, -1, 0, (int)reverse, X);
+                     x, n, n, (int)rows, (int)pairing, (int)nb, 0, 2, (int)reverse, X);
   int st = launch_status();
   if (st) return st;
-  const int64_t h_stride = per_row_kernel ? upols_partitions(klen) * kN : 0;
-  // UPOLS_MAC_BLK (25) output blocks per thread: each X row is re-read (Q+BLK-1)/BLK times through L2
-  // (A/B at config 2: 25 blocks 26.6 us vs 16 blocks 28.3 us, 8 and 32 no better)
-  // (measured slower: an LDS-tiled variant that reads X once, 25%: lower occupancy, exposed
-  // loads; every operand loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one
-  // thread per (pair, bin) streaming all blocks with a register ring, 8%)
-  constexpr int BLK = UPOLS_MAC_BLK;
-  hipLaunchKernelGGL(upols_mac_kernel<BLK>, dim3(kN / kNT, (unsigned)((nb + BLK - 1) / BLK), (unsigned)npairs),
-                     dim3(kNT), 0, S(stream), X, reinterpret_cast<const float2*>(spectrum), h_stride,
-                     (int)nb, (int)Q, Y);
-  if ((st = launch_status())) return st;
-  hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     Y, (int)nb, n, (int)rows, (int)pairing, (int)reverse, y, n);
-  return launch_status();
+  return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
 }
 
 size_t upols_spectra_bytes(int64_t rows, int64_t n) {
@@ -419,7 +426,7 @@ size_t upols_spectra_bytes(int64_t rows, int64_t n) {
 }
 
 size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x) {
-  const int64_t Q = upols_partitions(std::min(klen, n));
+  const int64_t Q = upols_kernel_windows(std::min(klen, n));
   const int64_t groups = corr_groups((rows + 1) / 2);
   return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)groups * Q * kN * sizeof(float2);
 }
@@ -429,7 +436,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   const int64_t npairs = (rows + 1) / 2;
   const int64_t nb = upols_blocks(n);
   const int64_t kc = std::min(klen, n);
-  const int64_t Q = upols_partitions(kc);
+  const int64_t Qp = upols_partitions(kc), Q = Qp + 1;  // output partitions of dimp; kernel windows
   const int64_t groups = corr_groups(npairs);
   const bool need_x = dimp && !x_spectra;
   if (!ws || ws_bytes < upols_backward_workspace_bytes(rows, n, klen, !need_x)) return DDSP_HIP_EWORKSPACE;
@@ -458,14 +465,14 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
     if (need_x) {
       if (!x) return DDSP_HIP_EINVAL;
       hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), x, n,
-                         n, (int)rows, 1, (int)nb, -1, 0, 0, Xs);
+                         n, (int)rows, 1, (int)nb, 0, 2, 0, Xs);
       if ((st = launch_status())) return st;
     }
     hipLaunchKernelGGL(upols_corr_kernel<8>, dim3(kN / 64, (unsigned)((Q + 7) / 8), (unsigned)groups),
                        dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
                        part);
     if ((st = launch_status())) return st;
-    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Q), dim3(kNT), 0, S(stream), part, (int)groups,
+    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), part, (int)groups,
                        (int)Q, kc, dimp);
     if ((st = launch_status())) return st;
   }
