@@ -56,6 +56,9 @@ __device__ __forceinline__ bool frame_synth(
 
   // ---- phase 1: independent loads and per-element work ----
   double part_s = 0.0, part_d = 0.0;
+#ifdef DDSP_PROBE_NO_PREFIX
+  if (false)
+#endif
   for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
   for (int k = tid; k < H; k += NT) {  // modules.py:53-60 before normalisation
     const float v = controls_value(prow[1 + k], pitch0, k, half_sr);

@@ -75,6 +75,18 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
 #ifndef UPOLS_MAC_BLK
 #define UPOLS_MAC_BLK 25
 #endif
+#ifndef UPOLS_MAC_RING
+#define UPOLS_MAC_RING 1
+#endif
+#ifndef UPOLS_RING_BLK
+#define UPOLS_RING_BLK 25
+#endif
+#ifndef UPOLS_RING_PF
+#define UPOLS_RING_PF 3
+#endif
+#ifndef UPOLS_RING_GR
+#define UPOLS_RING_GR 3
+#endif
 
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
@@ -177,6 +189,79 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
     const int bn = b0 - p - 1;
     const float2 xv = Xp[(int64_t)max(bn, 0) * kN];
     win[0] = bn >= 0 ? xv : zero;
+  }
+  float2* Yp = Y + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int d = 0; d < BLK; ++d)
+    if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
+}
+
+// 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
+// `bytes` records; offsets at or past `bytes` read as zero).  The row pointer and size are
+// wave-uniform, so the descriptor lives in SGPRs.
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+constexpr int kBufferWord3 = 0x00020000;  // gfx9 raw-buffer DATA_FORMAT word
+__device__ __forceinline__ float2 row_load(const float2* row, int bytes, int voff) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(row), (short)0, bytes, kBufferWord3);
+  const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  return make_float2(__int_as_float(v.x), __int_as_float(v.y));
+}
+
+// The same sums with the Z window as a register ring indexed statically.  The p loop is unrolled by
+// the ring size R = BLK + PF - 1, so the slot (m - b0) mod R of block m is a compile-time register
+// at every unrolled step and the window never shifts (no v_mov).  After step p's products, block
+// b0 - p - PF is loaded into the slot step p freed (block b0 + BLK - 1 - p), and G_{p+PF} into a
+// G ring of GR >= PF slots (GR | R): every operand is loaded PF steps before its first use.  The
+// unrolled rounds carry no per-step guards (guards made the compiler enter the round through a
+// jump table, whose joins forced a wait on every load at every step): steps past the last useful
+// one read the zero spectra of out-of-range descriptors (G_q, q >= Q; Z_m, m < 0) and add exact
+// zeros.  grid (N/256, ceil(nb/BLK), npairs)
+template <int BLK, int PF, int GR>
+__global__ void __launch_bounds__(kNT) upols_mac_ring_kernel(const float2* __restrict__ X,
+                                                             const float2* __restrict__ Hs,
+                                                             int64_t h_pair_stride, int nb, int Q,
+                                                             float2* __restrict__ Y) {
+  constexpr int R = BLK + PF - 1;
+  static_assert(PF >= 1 && R % GR == 0 && GR >= PF, "ring shapes");
+  constexpr int kRow = kN * (int)sizeof(float2);
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int b0 = nb - (int)(gridDim.y - blockIdx.y) * BLK;
+  const int pair = blockIdx.z;
+  // Every spectrum row is read through a buffer descriptor built in SGPRs for that row (base =
+  // the row, lane offset = 8 f): no per-lane address arithmetic, and rows outside the signal or
+  // the kernel are descriptors with no records, whose loads return 0 without a select.
+  const float2* Xrow = X + (int64_t)pair * nb * kN;
+  const float2* Hrow = Hs + (int64_t)pair * h_pair_stride;
+  const int voff = f * (int)sizeof(float2);
+  float2 ring[R], g[GR];
+  v2f acc[BLK];
+  auto zload = [&](int m, float2& dst) { dst = row_load(Xrow + (int64_t)max(m, 0) * kN, m >= 0 ? kRow : 0, voff); };
+  auto gload = [&](int q, float2& dst) { dst = row_load(Hrow + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+#pragma unroll
+  for (int d = 0; d < BLK; ++d) {
+    acc[d] = (v2f){0.f, 0.f};
+    zload(b0 + d, ring[d]);
+  }
+#pragma unroll
+  for (int j = 1; j < PF; ++j) zload(b0 - j, ring[R - j]);
+#pragma unroll
+  for (int j = 0; j < PF; ++j) gload(j, g[j]);
+  const int pmax = min(Q, b0 + BLK);
+  for (int pb = 0; pb < pmax; pb += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int p = pb + u;
+      const float2 h = g[u % GR];
+      const v2f hb = {h.x, h.y}, hr = {-h.y, h.x};
+#pragma unroll
+      for (int d = 0; d < BLK; ++d) cmac(acc[d], ring[(d - u + R) % R], hb, hr);
+      gload(p + PF, g[(u + PF) % GR]);
+      zload(b0 - p - PF, ring[(BLK - 1 - u + R) % R]);
+      // keep the scheduler from sinking the loads toward their uses (it did, to cut register
+      // live ranges, which turned the prefetch into a wait on every load)
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   float2* Yp = Y + (int64_t)pair * nb * kN + f;
 #pragma unroll
@@ -393,9 +478,16 @@ int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* s
   // an LDS-tiled variant that reads Z once, 25%: lower occupancy, exposed loads; every operand
   // loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one thread per (pair, bin)
   // streaming all blocks with a register ring, 8%)
+#if UPOLS_MAC_RING
+  constexpr int RB = UPOLS_RING_BLK;
+  hipLaunchKernelGGL((upols_mac_ring_kernel<RB, UPOLS_RING_PF, UPOLS_RING_GR>),
+                     dim3(kN / kNT, (unsigned)((nb + RB - 1) / RB), (unsigned)npairs), dim3(kNT), 0, S(stream), Z,
+                     reinterpret_cast<const float2*>(spectrum), h_stride, (int)nb, (int)Q, Y);
+#else
   hipLaunchKernelGGL(upols_mac_kernel<BLK>, dim3(kN / kNT, (unsigned)((nb + BLK - 1) / BLK), (unsigned)npairs),
                      dim3(kNT), 0, S(stream), Z, reinterpret_cast<const float2*>(spectrum), h_stride,
                      (int)nb, (int)Q, Y);
+#endif
   int st = launch_status();
   if (st) return st;
   hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),

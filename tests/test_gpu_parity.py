@@ -432,6 +432,25 @@ def test_config4_long_ir_reverb(dd):
     assert rms(out, ref) < 1e-6 * scale
 
 
+def test_config4_synth_path_end_to_end(dd):
+    """Config 4 end to end: B=16, F=200, H=100 through the fused synthesis and the 2 s reverb
+    (Reverb(96000, 48000): 48 kernel windows, more than the MAC's 25-block register window),
+    four items against the torch-CPU restatement of the reference."""
+    from ddsp_pytorch_amd.synth import make_inputs, SynthPath
+    inp = make_inputs(16, 200, 100, 65, 512, seed=4, device="cuda")
+    syn = SynthPath(512, 48000, reverb_length=96000, noise_mode="inject").cuda()
+    with torch.no_grad():
+        out = syn(inp["f0"], inp["param"], inp["mags"], inp["noise"])
+    rv = tr.Reverb(syn.reverb.noise.detach().cpu(), syn.reverb.decay.detach().cpu(),
+                   syn.reverb.wet.detach().cpu(), 96000, 48000)
+    sl = slice(0, 16, 5)
+    ref = tr.synth_path(inp["f0"][sl].cpu(), inp["param"][sl].cpu(), inp["mags"][sl].cpu(),
+                        inp["noise"][sl].cpu(), rv, 512, 48000).numpy()
+    got = C(out[sl])
+    for i in range(ref.shape[0]):
+        assert rms(got[i], ref[i]) < PARITY_RMS, (i, rms(got[i], ref[i]))
+
+
 def test_config5_synth_path_items(dd):
     """Config 5 shard shape: 400 frames, 128 harmonics (|arg| up to ~3.4e6 rad); two items of a
     64-item shard against the torch-CPU restatement of the reference."""
