@@ -40,8 +40,7 @@ constexpr int kPad = kN + kN / 16;  // LDS float2 slots: one pad slot per 16 (ba
 // Full 4096-point transform (three radix-16 Stockham passes, Ns = 1, 16, 256):
 // v holds in[j + 256 r] on entry and out[j + 256 r] on exit.
 template <bool INV>
-__device__ __forceinline__ void fft4096(float2 (&v)[16], float2* lds) {
-  const int j = threadIdx.x;
+__device__ __forceinline__ void fft4096(float2 (&v)[16], float2* lds, int j = threadIdx.x) {
   // pass twiddle steps: k * N/(Ns*16) with k = j mod Ns
   const Tw4 tw2 = load_tw<INV>((j & 15) * 16);
   const Tw4 tw3 = load_tw<INV>(j);
@@ -87,6 +86,9 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
 #ifndef UPOLS_RING_GR
 #define UPOLS_RING_GR 3
 #endif
+#ifndef UPOLS_RING_WAVES
+#define UPOLS_RING_WAVES 1
+#endif
 
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
@@ -123,10 +125,27 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
     const int64_t si = reverse ? T - 1 - s : s;
     v[r] = make_float2(ok ? xa[si] : 0.0f, (ok && xb) ? xb[si] : 0.0f);
   }
+#ifndef DDSP_PROBE_FWD_NOFFT
   fft4096<false>(v, lds);
+#endif
   float2* out = X + ((int64_t)pair * nb + b) * kN;
+#ifdef DDSP_PROBE_FWD_NOSTORE
+  if (v[3].x == 1234.5f)
+#endif
 #pragma unroll
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+}
+
+// 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
+// `bytes` records; offsets at or past `bytes` read as zero).  The row pointer and size are
+// wave-uniform, so the descriptor lives in SGPRs.
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+constexpr int kBufferWord3 = 0x00020000;  // gfx9 raw-buffer DATA_FORMAT word
+__device__ __forceinline__ float2 row_load(const float2* row, int bytes, int voff) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(row), (short)0, bytes, kBufferWord3);
+  const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  return make_float2(__int_as_float(v.x), __int_as_float(v.y));
 }
 
 // G[row][q][:] = FFT(h[row][(q-1)P, (q+1)P) (zero outside [0, klen))) / N, q = 0..Q;
@@ -196,18 +215,6 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
     if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
 }
 
-// 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
-// `bytes` records; offsets at or past `bytes` read as zero).  The row pointer and size are
-// wave-uniform, so the descriptor lives in SGPRs.
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-constexpr int kBufferWord3 = 0x00020000;  // gfx9 raw-buffer DATA_FORMAT word
-__device__ __forceinline__ float2 row_load(const float2* row, int bytes, int voff) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(row), (short)0, bytes, kBufferWord3);
-  const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
-  return make_float2(__int_as_float(v.x), __int_as_float(v.y));
-}
-
 // The same sums with the Z window as a register ring indexed statically.  The p loop is unrolled by
 // the ring size R = BLK + PF - 1, so the slot (m - b0) mod R of block m is a compile-time register
 // at every unrolled step and the window never shifts (no v_mov).  After step p's products, block
@@ -218,7 +225,7 @@ __device__ __forceinline__ float2 row_load(const float2* row, int bytes, int vof
 // one read the zero spectra of out-of-range descriptors (G_q, q >= Q; Z_m, m < 0) and add exact
 // zeros.  grid (N/256, ceil(nb/BLK), npairs)
 template <int BLK, int PF, int GR>
-__global__ void __launch_bounds__(kNT) upols_mac_ring_kernel(const float2* __restrict__ X,
+__global__ void __launch_bounds__(kNT, UPOLS_RING_WAVES) upols_mac_ring_kernel(const float2* __restrict__ X,
                                                              const float2* __restrict__ Hs,
                                                              int64_t h_pair_stride, int nb, int Q,
                                                              float2* __restrict__ Y) {
@@ -464,6 +471,17 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
   return launch_status();
 }
 
+// Z[pair][b] = FFT of block b of the packed rows with one half zeroed (zh: 2 = [x_b, 0], 1 = [0, x_b]).
+// (Measured slower: a persistent, software-pipelined variant that loads the next block under the
+// current transform, 20.5 us vs 18.7 at config 2 with 2 blocks per workgroup, 26 us with 6: each
+// transform is a ~4 us latency-bound chain of LDS passes, and fewer resident workgroups expose it.)
+static int launch_forward(const float* x, int64_t n, int64_t rows, int pairing, int64_t nb, int64_t npairs, int off,
+                          int zh, int reverse, float2* Z, void* stream) {
+  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), x, n, n,
+                     (int)rows, pairing, (int)nb, off, zh, reverse, Z);
+  return launch_status();
+}
+
 int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
                         bool per_row_kernel, float* y, float2* Y, void* stream, bool reverse) {
   const bool pairing = !per_row_kernel;
@@ -505,9 +523,7 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
   // Z_b = FFT([x_b, 0])
-  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
-                     x, n, n, (int)rows, (int)pairing, (int)nb, 0, 2, (int)reverse, X);
-  int st = launch_status();
+  int st = launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
   if (st) return st;
   return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
 }
@@ -541,9 +557,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   float2* Xs = need_x ? reinterpret_cast<float2*>(w + 2 * sb + (size_t)groups * Q * kN * sizeof(float2))
                       : const_cast<float2*>(reinterpret_cast<const float2*>(x_spectra));
   // GZ_b = F([0, g_b])
-  hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), g, n, n,
-                     (int)rows, 1, (int)nb, -1, 1, 0, GZ);
-  int st = launch_status();
+  int st = launch_forward(g, n, rows, 1, nb, npairs, -1, 1, 0, GZ, stream);
   if (st) return st;
   if (dx) {
     hipLaunchKernelGGL(upols_mac_adj_kernel<16>, dim3(kN / kNT, (unsigned)((nb + 15) / 16), (unsigned)npairs),
@@ -556,9 +570,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   if (dimp) {
     if (need_x) {
       if (!x) return DDSP_HIP_EINVAL;
-      hipLaunchKernelGGL(upols_forward_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), x, n,
-                         n, (int)rows, 1, (int)nb, 0, 2, 0, Xs);
-      if ((st = launch_status())) return st;
+      if ((st = launch_forward(x, n, rows, 1, nb, npairs, 0, 2, 0, Xs, stream))) return st;
     }
     hipLaunchKernelGGL(upols_corr_kernel<8>, dim3(kN / 64, (unsigned)((Q + 7) / 8), (unsigned)groups),
                        dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
