@@ -5,7 +5,7 @@ ARCH ?= gfx950
 SRC := ddsp_pytorch_amd/csrc/synth.hip ddsp_pytorch_amd/csrc/noise.hip ddsp_pytorch_amd/csrc/reverb.hip \
        ddsp_pytorch_amd/csrc/upols.hip ddsp_pytorch_amd/csrc/synth_frame.hip \
        ddsp_pytorch_amd/csrc/backward.hip ddsp_pytorch_amd/csrc/stft.hip \
-       ddsp_pytorch_amd/csrc/gru.hip ddsp_pytorch_amd/csrc/dense.hip
+       ddsp_pytorch_amd/csrc/gru.hip ddsp_pytorch_amd/csrc/dense.hip ddsp_pytorch_amd/csrc/stream.hip
 HDR := include/ddsp_hip.h ddsp_pytorch_amd/csrc/common.h ddsp_pytorch_amd/csrc/upols.h ddsp_pytorch_amd/csrc/fft_radix.h \
        ddsp_pytorch_amd/csrc/noise_dsp.h
 LIB := ddsp_pytorch_amd/lib/libddsp_hip.so

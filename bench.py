@@ -85,6 +85,10 @@ def parse():
                    help="PMC HBM bytes per launch (tools/pmc_traffic.py output)")
     p.add_argument("--valu-counts", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
                    help="PMC SQ_INSTS_VALU per launch of the dominant kernel (tools/pmc_valu.py output)")
+    p.add_argument("--no-pipelined-leg", action="store_true",
+                   help="skip the two-stage serving pipeline leg (synth.PipelinedSynthPath)")
+    p.add_argument("--reverb-cus", type=int, default=64,
+                   help="CUs of the pipelined leg's reverb partition (the rest run the synthesis)")
     p.add_argument("--no-uncached-leg", action="store_true",
                    help="skip the step with the IR spectrum rebuilt on every call (as modules.py:30-33)")
     a = p.parse_args()
@@ -415,6 +419,44 @@ def scatter_gather_leg(synth, held, global_batch, tails, samples_per_step, steps
             g)
 
 
+def pipelined_leg(syn, run_args, samples_per_step, steps, reverb_cus, dev, dist, warm=10):
+    """Serving form over consecutive batches (synth.PipelinedSynthPath): the synthesis of batch i+1
+    on one CU partition beside the reverb of batch i on the other.  Same work per batch as the
+    headline step; reported beside it, never as it.  Timed between barrier + device sync, max over
+    ranks; latency = one batch alone through both stages (best of 5)."""
+    from ddsp_pytorch_amd.synth import PipelinedSynthPath
+    pipe = PipelinedSynthPath(syn, reverb_cus=reverb_cus, device=dev)
+    for _ in range(warm):
+        pipe(*run_args)
+    pipe.join()
+    _sync(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipe(*run_args)
+    pipe.join()
+    _sync(dev)
+    t = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = _max_over_ranks(t, dev, dist)
+    lat = []
+    for _ in range(5):
+        _sync(dev)
+        t1 = time.perf_counter()
+        pipe(*run_args)
+        pipe.join()
+        _sync(dev)
+        lat.append(time.perf_counter() - t1)
+    return {"value": round(samples_per_step * steps / t, 1), "unit": "samples/s",
+            "ms_per_step": round(t / steps * 1e3, 4), "latency_ms": round(min(lat) * 1e3, 4),
+            "cu_split": {"reverb": reverb_cus, "synthesis": pipe.n_cu - reverb_cus},
+            "note": "two-stage pipeline over consecutive batches on CU-masked streams (synthesis of "
+                    "batch i+1 beside the reverb of batch i); same work per batch as the headline "
+                    "step, reported beside it"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -573,6 +615,14 @@ def main():
                                  "ms_per_step": round(tu / args.steps * 1e3, 4),
                                  "note": "step with the reverb IR and its partition spectra rebuilt every call "
                                          "(Reverb.cache_spectrum = False), as the reference's Reverb.forward does"}
+
+    if syn.reverb is not None and world == 1 and not args.no_pipelined_leg:
+        try:
+            result["pipelined"] = pipelined_leg(
+                syn, (inp["f0"], inp["param"], inp["mags"], inp.get("noise")), samples_per_step,
+                args.steps, args.reverb_cus, dev, dist)
+        except Exception as e:  # a refused CU mask must not cost the headline line
+            result["pipelined"] = {"error": f"{type(e).__name__}: {e}"}
 
     if dist and not args.no_gather:
         r, g = gathered_leg(step, B * world, samples_per_step, args.steps, dev, dist)

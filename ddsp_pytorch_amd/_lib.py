@@ -43,6 +43,8 @@ class DenseProblem(ctypes.Structure):
 SIGNATURES = {
     "ddsp_hip_status_string": (ctypes.c_char_p, [_I]),
     "ddsp_hip_version": (_I, []),
+    "ddsp_hip_stream_create_cu_masked": (_I, [ctypes.POINTER(ctypes.c_uint32), _I, ctypes.POINTER(_P)]),
+    "ddsp_hip_stream_destroy": (_I, [_P]),
     "ddsp_hip_scale_function": (_I, [_P, _P, _I64, _F, _P]),
     "ddsp_hip_remove_above_nyquist": (_I, [_P, _P, _P, _I64, _I64, _F, _P]),
     "ddsp_hip_upsample": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),

@@ -580,3 +580,27 @@ def _reverb_apply_launch(x, spectrum, ir_length):
 
 
 from . import grad as _grad  # noqa: E402  (autograd Functions over the backward kernels)
+
+
+_MASKED_STREAMS = {}
+
+
+def cu_masked_stream(cus, n_cu=None):
+    """A torch stream whose kernels run only on the CUs with the given indices
+    (ddsp_hip_stream_create_cu_masked; see synth.PipelinedSynthPath for how indices map to XCDs).
+    One stream per (device, mask), kept for the life of the process: the caching allocator may
+    still hold blocks tagged with it, so it is never destroyed under them."""
+    dev = torch.cuda.current_device()
+    cus = tuple(sorted(set(int(c) for c in cus)))
+    n_cu = n_cu or torch.cuda.get_device_properties(dev).multi_processor_count
+    if not cus or cus[0] < 0 or cus[-1] >= n_cu:
+        raise ValueError("CU indices out of range")
+    key = (dev, cus)
+    if key not in _MASKED_STREAMS:
+        words = (ctypes.c_uint32 * ((n_cu + 31) // 32))()
+        for c in cus:
+            words[c // 32] |= 1 << (c % 32)
+        handle = ctypes.c_void_p()
+        _lib.call("stream_create_cu_masked", words, len(words), ctypes.byref(handle))
+        _MASKED_STREAMS[key] = torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", dev))
+    return _MASKED_STREAMS[key]

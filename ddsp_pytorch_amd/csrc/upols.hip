@@ -71,6 +71,9 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
   acc = __builtin_elementwise_fma((v2f){a.y, a.y}, b_rot, acc);
 }
 
+// MAC variants, compile-time (tools/ab_build.sh -D...): the shipped MAC is the register-ring kernel
+// (UPOLS_MAC_RING=1, 25 blocks, prefetch 3, G ring 3); UPOLS_MAC_RING=0 builds the shifting-window
+// kernel it replaced (29.3 vs 25.7-26.7 us at config 2), kept as the A/B baseline
 #ifndef UPOLS_MAC_BLK
 #define UPOLS_MAC_BLK 25
 #endif

@@ -341,6 +341,14 @@ int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, con
                                      float sample_rate, float* grad_noise, float* grad_decay, float* grad_wet,
                                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* Two-stage serving pipeline (ddsp_pytorch_amd.synth.PipelinedSynthPath; no reference counterpart:
+ * the reference synthesises one batch at a time, decoder.py:101-136).  A HIP stream restricted to
+ * the CUs whose bits are set in cu_mask (mask_words 32-bit words, bit c = CU index c; HIP deals
+ * consecutive indices over the XCDs).  DDSP_HIP_ELAUNCH if the runtime refuses the mask.  The
+ * caller owns the stream and releases it with ddsp_hip_stream_destroy. */
+int ddsp_hip_stream_create_cu_masked(const uint32_t* cu_mask, int mask_words, void** stream);
+int ddsp_hip_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif
