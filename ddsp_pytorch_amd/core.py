@@ -13,6 +13,7 @@ Besides the six reference functions, the fused frame-rate ops used by the module
 drop-ins (``modules.py``) live here: ``harmonic_controls``, ``harmonic_synth_frames``,
 ``filtered_noise``, ``reverb_build_impulse``, ``reverb_spectrum``, ``reverb_apply``.
 """
+import atexit
 import ctypes
 import itertools
 import math
@@ -583,6 +584,22 @@ from . import grad as _grad  # noqa: E402  (autograd Functions over the backward
 
 
 _MASKED_STREAMS = {}
+
+
+@atexit.register
+def _release_masked_streams():
+    """Destroy the CU-masked streams before the HIP runtime tears down (left to the runtime's own
+    teardown they crashed rocprofv3's finalisation)."""
+    if not _MASKED_STREAMS:
+        return
+    try:
+        torch.cuda.synchronize()
+        lib = _lib.load()
+        for s in _MASKED_STREAMS.values():
+            lib.ddsp_hip_stream_destroy(s.cuda_stream)
+    except Exception:  # teardown path: nothing left to report to
+        pass
+    _MASKED_STREAMS.clear()
 
 
 def cu_masked_stream(cus, n_cu=None):

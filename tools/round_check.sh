@@ -28,4 +28,6 @@ step profile
 bash tools/profile.sh $TAG || exit 1
 step pmc-reverb
 bash tools/pmc_probe.sh reverb $TAG || exit 1
+step pmc-fused
+bash tools/pmc_probe.sh fused $TAG || exit 1
 echo round check $TAG done
