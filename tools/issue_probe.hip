@@ -114,6 +114,15 @@ __global__ void __launch_bounds__(512) mix(float* out, unsigned long long* cyc, 
           "v_sin_f32 %0, %0\n v_sin_f32 %1, %1\n v_sin_f32 %2, %2\n v_sin_f32 %3, %3\n"
           " v_sin_f32 %4, %4\n v_sin_f32 %5, %5\n v_sin_f32 %6, %6\n v_sin_f32 %7, %7\n"
           : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+  } else if (kind == 4) {  // bf16 MFMA chains (v_mfma_f32_16x16x32_bf16): the matrix core proper
+    typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+    bf8 x = {(__bf16)a0, (__bf16)a1, (__bf16)a2, (__bf16)a3, (__bf16)a4, (__bf16)a5, (__bf16)a6, (__bf16)a7};
+    for (int it = 0; it < ITER / 4; ++it) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, c3, 0, 0, 0);
+    }
   } else if (kind == 1) {
     for (int it = 0; it < ITER / 4; ++it) {
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, a1, c0, 0, 0, 0);
@@ -208,5 +217,8 @@ int main() {
   run_mix<0, 1>("fma | mfma (one of each per SIMD)", cus);
   run_mix<0, 0>("fma | fma", cus);
   run_mix<1, 1>("mfma | mfma", cus);
+  run_mix<4, 2>("mfma bf16 x4 waves | idle", cus);
+  run_mix<0, 4>("fma | mfma bf16", cus);
+  run_mix<3, 4>("sin | mfma bf16", cus);
   return 0;
 }
