@@ -419,11 +419,13 @@ def scatter_gather_leg(synth, held, global_batch, tails, samples_per_step, steps
             g)
 
 
-def pipelined_leg(syn, run_args, samples_per_step, steps, reverb_cus, dev, dist, warm=10):
+def pipelined_leg(syn, run_args, samples_per_step, steps, reverb_cus, dev, dist, warm=40):
     """Serving form over consecutive batches (synth.PipelinedSynthPath): the synthesis of batch i+1
     on one CU partition beside the reverb of batch i on the other.  Same work per batch as the
     headline step; reported beside it, never as it.  Timed between barrier + device sync, max over
-    ranks; latency = one batch alone through both stages (best of 5)."""
+    ranks; latency = one batch alone through both stages (best of 5).  The warmup runs until the
+    caching allocator holds the blocks the two streams cycle through (fresh blocks are hipMalloc'd
+    while signals still wait for the reverb stream: the first ~10-20 batches run slower)."""
     from ddsp_pytorch_amd.synth import PipelinedSynthPath
     pipe = PipelinedSynthPath(syn, reverb_cus=reverb_cus, device=dev)
     for _ in range(warm):

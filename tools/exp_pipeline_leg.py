@@ -12,7 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddsp_pytorch_amd import core  # noqa: E402
-from ddsp_pytorch_amd.synth import PipelinedSynthPath, SynthPath, make_inputs  # noqa: E402
+from ddsp_pytorch_amd.synth import PipelinedSynthPath, SynthGraph, SynthPath, make_inputs  # noqa: E402
 
 N = 100
 
@@ -38,8 +38,11 @@ def main():
     syn = SynthPath(bs, 48000, reverb_length=48000).cuda()
     args = (inp["f0"], inp["param"], inp["mags"], None)
     print(f"one stream: {timed(lambda: syn(*args)):6.1f} us", flush=True)
-    sa = core.cu_masked_stream(range(64, 256))
-    sb = core.cu_masked_stream(range(64))
+    pipe = PipelinedSynthPath(syn)
+    cur = torch.cuda.current_stream()
+    print("current is default:", cur == torch.cuda.default_stream(cur.device), cur, flush=True)
+    print(f"PipelinedSynthPath: {timed(lambda: pipe(*args), pipe.join):6.1f} us", flush=True)
+    sa, sb = pipe.s_synth, pipe.s_reverb
     spec = syn.reverb._spectrum(F * bs)
 
     def inline(use_module):
@@ -57,8 +60,13 @@ def main():
 
     print(f"inline, reverb_apply: {timed(lambda: inline(False)):6.1f} us", flush=True)
     print(f"inline, Reverb module: {timed(lambda: inline(True)):6.1f} us", flush=True)
-    pipe = PipelinedSynthPath(syn)
-    print(f"PipelinedSynthPath: {timed(lambda: pipe(*args), pipe.join):6.1f} us", flush=True)
+    print(f"PipelinedSynthPath again: {timed(lambda: pipe(*args), pipe.join):6.1f} us", flush=True)
+    g = SynthGraph(syn, inp["f0"], inp["param"], inp["mags"])
+    print(f"one stream, HIP graph replay: {timed(g.replay):6.1f} us", flush=True)
+    cur = torch.cuda.current_stream()
+    print("current is default:", cur == torch.cuda.default_stream(cur.device), cur, flush=True)
+    print(f"PipelinedSynthPath after the graph: {timed(lambda: pipe(*args), pipe.join):6.1f} us", flush=True)
+    print(f"one stream again: {timed(lambda: syn(*args)):6.1f} us", flush=True)
 
 
 if __name__ == "__main__":
