@@ -14,7 +14,7 @@
 //   overlap by half (q = 0..Q, Q = ceil(L/P), h_{-1} = h_Q = 0):
 //   kernel:   G_q = FFT_N([h_{q-1}, h_q]) / N                   (computed once per IR)
 //   forward:  Z_b = FFT_N([x_b, 0])                             (upols_forward_kernel)
-//   MAC:      Y_b = sum_{q=0..Q} Z_{b-q} G_q   per frequency bin (upols_mac_kernel)
+//   MAC:      Y_b = sum_{q=0..Q} Z_{b-q} G_q   per frequency bin (upols_mac_ring_kernel)
 //   inverse:  y[bP, (b+1)P) = last P points of IFFT_N(Y_b)      (upols_inverse_kernel)
 //   (circular convolution of [x_{b-q}, 0] with [h_{q-1}, h_q]: its second half holds exactly the
 //   terms h[tau] x[bP + n - tau] with tau in ((q-1)P + n, qP + n], so the Q+1 terms cover every
@@ -410,6 +410,57 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __rest
     if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(sgn * acc[d].x, sgn * acc[d].y);
 }
 
+// The adjoint MAC on the forward MAC's register ring: the window over GZ_{j0+d+q} (d < BLK) slides
+// forward, so block m sits in slot (m - j0) mod R (R = BLK + PF - 1), step u of a round reads slot
+// (d + u) mod R, and after its products block j0 + q + BLK + PF - 1 is loaded into the slot step q
+// freed (block j0 + q).  Blocks past the signal and windows past the kernel are descriptors with
+// no records (zeros), so the unrolled rounds carry no guards.  grid (N/256, ceil(nb/BLK), npairs)
+template <int BLK, int PF, int GR>
+__global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* __restrict__ G,
+                                                                 const float2* __restrict__ Hs, int nb, int Q,
+                                                                 float2* __restrict__ V) {
+  constexpr int R = BLK + PF - 1;
+  static_assert(PF >= 1 && R % GR == 0 && GR >= PF, "ring shapes");
+  constexpr int kRow = kN * (int)sizeof(float2);
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int j0 = blockIdx.y * BLK;
+  const int pair = blockIdx.z;
+  const float2* Grow = G + (int64_t)pair * nb * kN;
+  const int voff = f * (int)sizeof(float2);
+  float2 ring[R], g[GR];
+  v2f acc[BLK];
+  auto zload = [&](int m, float2& dst) { dst = row_load(Grow + (int64_t)min(m, nb - 1) * kN, m < nb ? kRow : 0, voff); };
+  auto hload = [&](int q, float2& dst) { dst = row_load(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+#pragma unroll
+  for (int d = 0; d < BLK; ++d) {
+    acc[d] = (v2f){0.f, 0.f};
+    zload(j0 + d, ring[d]);
+  }
+#pragma unroll
+  for (int i = BLK; i < R; ++i) zload(j0 + i, ring[i]);
+#pragma unroll
+  for (int i = 0; i < PF; ++i) hload(i, g[i]);
+  const int qmax = min(Q, nb - j0);
+  for (int qb = 0; qb < qmax; qb += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int q = qb + u;
+      const float2 h = g[u % GR];
+      const v2f hc = {h.x, -h.y}, hcr = {h.y, h.x};  // conj(h) and its rotation
+#pragma unroll
+      for (int d = 0; d < BLK; ++d) cmac(acc[d], ring[(d + u) % R], hc, hcr);
+      hload(q + PF, g[(u + PF) % GR]);
+      zload(j0 + q + R, ring[u]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of its use (see the forward MAC)
+    }
+  }
+  const float sgn = (f & 1) ? -1.0f : 1.0f;
+  float2* Vp = V + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int d = 0; d < BLK; ++d)
+    if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(sgn * acc[d].x, sgn * acc[d].y);
+}
+
 // dimp[pP + n] = Re(IFFT(sum_groups part[grp][p] + (-1)^f part[grp][p+1])) [P + n] / N for n < P,
 // pP + n < klen (part holds Q + 1 lags; lag Q + 1 is zero); grid (Q)
 __global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __restrict__ part, int groups,
@@ -563,8 +614,15 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   int st = launch_forward(g, n, rows, 1, nb, npairs, -1, 1, 0, GZ, stream);
   if (st) return st;
   if (dx) {
+#if UPOLS_MAC_RING
+    constexpr int AB = UPOLS_RING_BLK;
+    hipLaunchKernelGGL((upols_mac_adj_ring_kernel<AB, UPOLS_RING_PF, UPOLS_RING_GR>),
+                       dim3(kN / kNT, (unsigned)((nb + AB - 1) / AB), (unsigned)npairs), dim3(kNT), 0, S(stream), GZ,
+                       reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
+#else
     hipLaunchKernelGGL(upols_mac_adj_kernel<16>, dim3(kN / kNT, (unsigned)((nb + 15) / 16), (unsigned)npairs),
                        dim3(kNT), 0, S(stream), GZ, reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
+#endif
     if ((st = launch_status())) return st;
     hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), V,
                        (int)nb, n, (int)rows, 1, 0, dx, n);
