@@ -462,27 +462,36 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* _
 }
 
 // dimp[pP + n] = Re(IFFT(sum_groups part[grp][p] + (-1)^f part[grp][p+1])) [P + n] / N for n < P,
-// pP + n < klen (part holds Q + 1 lags; lag Q + 1 is zero); grid (Q)
-__global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __restrict__ part, int groups,
-                                                                int QG, int64_t klen, float* __restrict__ dimp) {
+// pP + n < klen (part holds Q + 1 lags; lag Q + 1 is zero), in two kernels:
+// sum[p][f] = sum_groups part[grp][p][f] + (-1)^f part[grp][p+1][f] (lag Q + 1 is zero): the group
+// reduction spread over the chip (grid (N/256, Qp)) so that the per-lag transform below reads one
+// spectrum (with the sum inside the 24 one-lag workgroups, each read 8 groups' spectra alone:
+// 14.5 us, per-CU bandwidth)
+__global__ void __launch_bounds__(kNT) upols_corr_sum_kernel(const float2* __restrict__ part, int groups, int QG,
+                                                             float2* __restrict__ sum) {
+  const int f = blockIdx.x * kNT + threadIdx.x, p = blockIdx.y;
+  const bool next = p + 1 < QG;
+  const float sg = (f & 1) ? -1.0f : 1.0f;
+  float2 v = make_float2(0.f, 0.f);
+  for (int g = 0; g < groups; ++g) {
+    const float2* in = part + ((int64_t)g * QG + p) * kN + f;
+    const float2 w = in[0];
+    const float2 w1 = next ? in[kN] : make_float2(0.f, 0.f);
+    v.x += w.x + sg * w1.x;
+    v.y += w.y + sg * w1.y;
+  }
+  sum[(int64_t)p * kN + f] = v;
+}
+
+// dimp[pP + n] = Re(IFFT(sum[p]))[P + n] / N for n < P, pP + n < klen; grid (Qp)
+__global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __restrict__ sum, int64_t klen,
+                                                                float* __restrict__ dimp) {
   __shared__ float2 lds[kPad];
   const int p = blockIdx.x, j = threadIdx.x;
+  const float2* in = sum + (int64_t)p * kN;
   float2 v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = make_float2(0.f, 0.f);
-  for (int g = 0; g < groups; ++g) {
-    const float2* in = part + ((int64_t)g * QG + p) * kN;
-    const bool next = p + 1 < QG;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int f = j + 256 * r;
-      const float2 w = in[f];
-      const float2 w1 = next ? in[kN + f] : make_float2(0.f, 0.f);
-      const float sg = (f & 1) ? -1.0f : 1.0f;
-      v[r].x += w.x + sg * w1.x;
-      v[r].y += w.y + sg * w1.y;
-    }
-  }
+  for (int r = 0; r < 16; ++r) v[r] = in[j + 256 * r];
   fft4096<true>(v, lds);
   const float inv_n = 1.0f / (float)kN;
 #pragma unroll
@@ -590,7 +599,7 @@ size_t upols_spectra_bytes(int64_t rows, int64_t n) {
 size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x) {
   const int64_t Q = upols_kernel_windows(std::min(klen, n));
   const int64_t groups = corr_groups((rows + 1) / 2);
-  return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)groups * Q * kN * sizeof(float2);
+  return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)(groups + 1) * Q * kN * sizeof(float2);
 }
 
 int upols_backward(const float* x, const float* x_spectra, const float* spectrum, const float* g, int64_t rows,
@@ -608,7 +617,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   float2* GZ = reinterpret_cast<float2*>(w);
   float2* V = reinterpret_cast<float2*>(w + sb);
   float2* part = reinterpret_cast<float2*>(w + 2 * sb);
-  float2* Xs = need_x ? reinterpret_cast<float2*>(w + 2 * sb + (size_t)groups * Q * kN * sizeof(float2))
+  float2* Xs = need_x ? reinterpret_cast<float2*>(w + 2 * sb + (size_t)(groups + 1) * Q * kN * sizeof(float2))
                       : const_cast<float2*>(reinterpret_cast<const float2*>(x_spectra));
   // GZ_b = F([0, g_b])
   int st = launch_forward(g, n, rows, 1, nb, npairs, -1, 1, 0, GZ, stream);
@@ -637,8 +646,11 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
                        dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
                        part);
     if ((st = launch_status())) return st;
-    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), part, (int)groups,
-                       (int)Q, kc, dimp);
+    float2* psum = part + (size_t)groups * Q * kN;
+    hipLaunchKernelGGL(upols_corr_sum_kernel, dim3(kN / kNT, (unsigned)Qp), dim3(kNT), 0, S(stream), part,
+                       (int)groups, (int)Q, psum);
+    if ((st = launch_status())) return st;
+    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), psum, kc, dimp);
     if ((st = launch_status())) return st;
   }
   return DDSP_HIP_OK;
