@@ -668,17 +668,23 @@ int ddsp_hip_synth_frames_backward(const float* f0, const float* param, const fl
   if (batch == 0 || frames == 0) return batch < 0 || frames < 0 ? DDSP_HIP_EINVAL : DDSP_HIP_OK;
   if (!f0 || !param || !raw_magnitudes || !grad_harmonic || !grad_param || !grad_magnitudes)
     return DDSP_HIP_EINVAL;
-  if (grad_noise && grad_noise != grad_harmonic) {  // distinct upstream gradients: two passes
-    int st = frame_backward_launch(2, 0, false, f0, grad_harmonic, param, nullptr, nullptr, grad_param, nullptr,
-                                   nullptr, batch, frames, n_harmonic, block_size, sample_rate, nullptr, nullptr, 0,
-                                   0, 0.0f, nullptr, 0, stream);
-    if (st) return st;
-    return ddsp_hip_filtered_noise_backward(raw_magnitudes, noise, seed, offset, 1, bias, grad_noise,
-                                            grad_magnitudes, batch, frames, n_bands, block_size, stream);
-  }
-  return frame_backward_launch(2, noise ? 1 : 2, true, f0, grad_harmonic, param, nullptr, nullptr, grad_param,
-                               nullptr, nullptr, batch, frames, n_harmonic, block_size, sample_rate, raw_magnitudes,
-                               noise, seed, offset, bias, grad_magnitudes, n_bands, stream);
+  // The two halves as two launches on the stream: measured faster than the one-launch form whose
+  // extra wave ran the noise VJP beside the sine waves (config 2, tools/exp_bwd_split.py: 176.7 vs
+  // 187.6-190.3 us; the halves alone 130.4 and 47.9 us, on two streams 223 us).  That form stays
+  // reachable as DDSP_BWD_FUSED for A/B.
+#ifdef DDSP_BWD_FUSED
+  if (!grad_noise || grad_noise == grad_harmonic)
+    return frame_backward_launch(2, noise ? 1 : 2, true, f0, grad_harmonic, param, nullptr, nullptr, grad_param,
+                                 nullptr, nullptr, batch, frames, n_harmonic, block_size, sample_rate,
+                                 raw_magnitudes, noise, seed, offset, bias, grad_magnitudes, n_bands, stream);
+#endif
+  int st = frame_backward_launch(2, 0, false, f0, grad_harmonic, param, nullptr, nullptr, grad_param, nullptr,
+                                 nullptr, batch, frames, n_harmonic, block_size, sample_rate, nullptr, nullptr, 0,
+                                 0, 0.0f, nullptr, 0, stream);
+  if (st) return st;
+  return ddsp_hip_filtered_noise_backward(raw_magnitudes, noise, seed, offset, 1, bias,
+                                          grad_noise ? grad_noise : grad_harmonic, grad_magnitudes, batch, frames,
+                                          n_bands, block_size, stream);
 }
 
 int ddsp_hip_filtered_noise_backward(const float* magnitudes, const float* noise, uint64_t seed, uint64_t offset,

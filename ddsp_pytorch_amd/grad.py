@@ -288,7 +288,7 @@ class SynthFramesFn(_F):
         NB = mags.shape[-1]
         dp = torch.empty(B, F, H1, dtype=torch.float32, device=param.device)
         dm = torch.empty(B, F, NB, dtype=torch.float32, device=param.device)
-        # one launch for both halves (the noise VJP fused into the harmonic one)
+        # both halves in one C-ABI call (two launches: harmonic, then noise VJP)
         _lib.call("synth_frames_backward", _lib.ptr(core._c(f0.detach())), _lib.ptr(core._c(param.detach())),
                   _lib.ptr(core._c(mags.detach())), ctx.bias, _lib.ptr(ctx.noise), ctx.seed, ctx.offset,
                   _lib.ptr(gh), _lib.ptr(gn), _lib.ptr(dp), _lib.ptr(dm), B, F, H1 - 1, NB, ctx.bs, ctx.sr,

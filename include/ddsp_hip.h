@@ -297,8 +297,8 @@ int ddsp_hip_harmonic_synth_params_backward(const float* f0, const float* param,
                                             int64_t n_harmonic, int64_t block_size, float sample_rate,
                                             void* stream);
 
-/* decoder.py:106-121 backward (ddsp_hip_synth_frames): one launch computes grad_param[B,F,H+1] and
- * grad_magnitudes[B,F,NB] (raw projections) from the upstream gradient of the signal; the noise
+/* decoder.py:106-121 backward (ddsp_hip_synth_frames): grad_param[B,F,H+1] and grad_magnitudes[B,F,NB]
+ * (raw projections) from the upstream gradient of the signal, as two launches (harmonic, noise); the noise
  * is `noise` or the forward's Philox (seed, offset).  grad_noise (nullable) is a separate upstream
  * gradient for the noise half (when the parts are used separately); NULL = grad_harmonic. */
 int ddsp_hip_synth_frames_backward(const float* f0, const float* param, const float* raw_magnitudes, float bias,

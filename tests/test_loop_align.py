@@ -14,10 +14,12 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 LIB = os.path.join(ROOT, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")
 
 # the throughput instantiations (one wave owns 4 samples x all harmonics): device-noise and
-# injected-noise forward, harmonic-only backward.  The one-sample-per-thread SPLIT forms run only
-# for launches of few frames (the realtime stream), which are latency-bound: reported, not pinned.
+# injected-noise forward, the harmonic half of the synthesis backward (the training step's
+# kernel since the backward runs as two launches) and the frame-control harmonic backward.  The
+# one-sample-per-thread SPLIT forms run only for launches of few frames (the realtime stream),
+# which are latency-bound: reported, not pinned.
 PINNED = ("synth_frame_kernelILb1ELb0EE", "synth_frame_kernelILb0ELb0EE",
-          "frame_backward_kernelILi2ELi2ELb1EE")
+          "frame_backward_kernelILi2ELi0ELb0EE", "frame_backward_kernelILi1ELi0ELb0EE")
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libddsp_hip.so not built (make)")
