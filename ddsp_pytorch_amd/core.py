@@ -602,6 +602,18 @@ def _release_masked_streams():
     _MASKED_STREAMS.clear()
 
 
+def cu_mask_words(cus, n_cu):
+    """The 32-bit mask words of ddsp_hip_stream_create_cu_masked: bit c of word c // 32 set for
+    every CU index c in ``cus`` (indices must lie in [0, n_cu))."""
+    words = [0] * ((int(n_cu) + 31) // 32)
+    for c in cus:
+        c = int(c)
+        if not 0 <= c < n_cu:
+            raise ValueError(f"CU index {c} outside [0, {n_cu})")
+        words[c // 32] |= 1 << (c % 32)
+    return words
+
+
 def cu_masked_stream(cus, n_cu=None):
     """A torch stream whose kernels run only on the CUs with the given indices
     (ddsp_hip_stream_create_cu_masked; see synth.PipelinedSynthPath for how indices map to XCDs).
@@ -614,9 +626,7 @@ def cu_masked_stream(cus, n_cu=None):
         raise ValueError("CU indices out of range")
     key = (dev, cus)
     if key not in _MASKED_STREAMS:
-        words = (ctypes.c_uint32 * ((n_cu + 31) // 32))()
-        for c in cus:
-            words[c // 32] |= 1 << (c % 32)
+        words = (ctypes.c_uint32 * ((n_cu + 31) // 32))(*cu_mask_words(cus, n_cu))
         handle = ctypes.c_void_p()
         _lib.call("stream_create_cu_masked", words, len(words), ctypes.byref(handle))
         _MASKED_STREAMS[key] = torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", dev))
