@@ -106,3 +106,19 @@ def test_pipelined_from_a_side_stream():
     torch.cuda.synchronize()
     assert all(torch.equal(g, r) for g, r in zip(got, ref))
 
+
+
+@pytest.mark.parametrize("B,F,H,NB,bs,L", [(1, 12, 40, 33, 256, 48000), (3, 10, 17, 9, 441, 2000)])
+def test_pipelined_odd_shapes(B, F, H, NB, bs, L):
+    """Batch of one and an odd batch; a block size outside the fused kernel's envelope (441: the
+    two-kernel fallback) and a reverb longer than the signal (the crop case, modules.py:30-33)."""
+    from ddsp_pytorch_amd.synth import PipelinedSynthPath, SynthPath, make_inputs
+    batches = [make_inputs(B, F, H, NB, bs, seed=40 + i, device="cuda") for i in range(3)]
+    syn = SynthPath(bs, 48000, reverb_length=L, noise_mode="inject").cuda()
+    ref = [syn(b["f0"], b["param"], b["mags"], b["noise"]).clone() for b in batches]
+    pipe = PipelinedSynthPath(syn)
+    outs = [pipe(b["f0"], b["param"], b["mags"], b["noise"]) for b in batches]
+    pipe.join()
+    torch.cuda.synchronize()
+    for i, (o, r) in enumerate(zip(outs, ref)):
+        assert o.shape == (B, F * bs, 1) and torch.equal(o, r), i
