@@ -642,9 +642,16 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
       if (!x) return DDSP_HIP_EINVAL;
       if ((st = launch_forward(x, n, rows, 1, nb, npairs, 0, 2, 0, Xs, stream))) return st;
     }
-    hipLaunchKernelGGL(upols_corr_kernel<8>, dim3(kN / 64, (unsigned)((Q + 7) / 8), (unsigned)groups),
-                       dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
-                       part);
+    // Every pass over the spectra covers PC lags, so the fewest passes win: PC = 13 up to 13 kernel
+    // windows, else 25 (Q = 25 at config 2: 8 lags per pass, 37.1 us -> 13, 26.8 -> 25, 24.7-25.0 us;
+    // 25 lags with 2 waves per workgroup and 16 groups 26.3, 1 wave and 32 groups 28.2)
+    if (Q <= 13)
+      hipLaunchKernelGGL(upols_corr_kernel<13>, dim3(kN / 64, 1, (unsigned)groups), dim3(64 * kCorrSlices), 0,
+                         S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups, part);
+    else
+      hipLaunchKernelGGL(upols_corr_kernel<25>, dim3(kN / 64, (unsigned)((Q + 24) / 25), (unsigned)groups),
+                         dim3(64 * kCorrSlices), 0, S(stream), Xs, GZ, (int)nb, (int)Q, (int)npairs, (int)groups,
+                         part);
     if ((st = launch_status())) return st;
     float2* psum = part + (size_t)groups * Q * kN;
     hipLaunchKernelGGL(upols_corr_sum_kernel, dim3(kN / kNT, (unsigned)Qp), dim3(kNT), 0, S(stream), part,

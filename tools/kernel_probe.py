@@ -1,6 +1,6 @@
 """Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
 
-    python tools/kernel_probe.py {fused,bwd,harmonic,harmonic_frames,noise,reverb,op} [reps]
+    python tools/kernel_probe.py {fused,bwd,reverb_bwd,harmonic,harmonic_frames,noise,reverb,op} [reps]
 """
 import os
 import sys
@@ -26,6 +26,13 @@ def main():
         g = torch.randn_like(out)
         for _ in range(reps):
             out.backward(g, retain_graph=True)
+        torch.cuda.synchronize()
+        return
+    if which == "reverb_bwd":  # the UPOLS backward (input and IR gradients)
+        x = torch.randn(B, F * bs, 1, device=dev, requires_grad=True)
+        g = torch.randn(B, F * bs, 1, device=dev)
+        for _ in range(reps):  # forward each time: the backward releases the kept input spectra
+            syn.reverb(x).backward(g)
         torch.cuda.synchronize()
         return
     with torch.no_grad():
