@@ -44,6 +44,20 @@ SIN_SLOTS = 4
 OSC_SLOTS_PER_SINE = 6 + SIN_SLOTS         # per (sample, harmonic): 6 fp32 VALU ops + one v_sin_f32
                                            # (synth_frame.hip inner loop; tools/loop_align.py counts it)
 
+KERNEL_SOURCES = ("ddsp_pytorch_amd/csrc/synth_frame.hip", "ddsp_pytorch_amd/csrc/common.h",
+                  "ddsp_pytorch_amd/csrc/noise_dsp.h")
+
+
+def kernel_source_sha():
+    """sha256 (16 hex) of the fused synthesis kernel's sources: PMC instruction counts recorded for
+    other sources (profiles/pmc_valu.json "source_sha") are stale and not used."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 
 def parse():
     p = argparse.ArgumentParser()
@@ -145,10 +159,11 @@ def cpu_baseline(args, rank_inputs_seed=0):
     """The reference's algorithm on the host cores: oracle/torch_ref.py (the same ATen op
     sequence as ddsp/core.py + modules.py, bit-exact to the reference's goldens).
 
-    Thread counts (BASELINE.md's plan: torch.set_num_threads(os.cpu_count())): the sample is
-    timed at os.cpu_count() threads and at the process's CPU share (OMP_NUM_THREADS / the
-    affinity mask; a GPU box gives one process a 16-core share of a larger host), and the faster
-    of the two is reported, with both timings and the host's core count."""
+    Thread counts (BASELINE.md's plan: torch.set_num_threads(os.cpu_count())): a sweep over
+    {16, 32, 64, 128, 256} threads capped at os.cpu_count(), plus the process's CPU share
+    (OMP_NUM_THREADS / the affinity mask; a GPU box gives one process a 16-core share of a larger
+    host), each timed on a 4-item sample; the fastest thread count is then timed on the full
+    sample and reported, with every sweep point and the host's core count."""
     from oracle import torch_ref as tr
     from ddsp_pytorch_amd.synth import make_inputs
     host = os.cpu_count() or 1
@@ -157,39 +172,49 @@ def cpu_baseline(args, rank_inputs_seed=0):
     except AttributeError:
         affinity = host
     share = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
-    B = args.cpu_batch
-    inp = make_inputs(B, args.frames, args.harmonics, args.bands, args.block_size, seed=0)
     torch.manual_seed(1)
     noise = (torch.rand(args.reverb_length) * 2 - 1).unsqueeze(-1)
     rv = tr.Reverb(noise, torch.tensor(5.0), torch.tensor(0.0), args.reverb_length, args.sample_rate)
-    run = lambda: tr.synth_path(inp["f0"], inp["param"], inp["mags"], inp["noise"], rv,
-                                args.block_size, args.sample_rate)
-    samples = B * args.frames * args.block_size
-    timed = {}
+
+    def runner(B):
+        inp = make_inputs(B, args.frames, args.harmonics, args.bands, args.block_size, seed=0)
+        return lambda: tr.synth_path(inp["f0"], inp["param"], inp["mags"], inp["noise"], rv,
+                                     args.block_size, args.sample_rate)
+
     prev = torch.get_num_threads()
-    for threads in sorted({host, share}):
+    sweep_b = min(4, args.cpu_batch)
+    run = runner(sweep_b)
+    by_threads = {}
+    for threads in sorted({t for t in (16, 32, 64, 128, 256) if t <= host} | {share}):
         torch.set_num_threads(threads)
         run()  # warm-up
-        times = []
-        budget = time.perf_counter() + 15.0
-        for _ in range(args.cpu_reps):
-            t0 = time.perf_counter()
-            run()
-            times.append(time.perf_counter() - t0)
-            if time.perf_counter() > budget:
-                break
-        timed[threads] = (sorted(times)[len(times) // 2], len(times))
+        t0 = time.perf_counter()
+        run()
+        by_threads[threads] = sweep_b * args.frames * args.block_size / (time.perf_counter() - t0)
+    best = max(by_threads, key=by_threads.get)
+    torch.set_num_threads(best)
+    B = args.cpu_batch
+    run = runner(B)
+    run()  # warm-up
+    times = []
+    budget = time.perf_counter() + 15.0
+    for _ in range(args.cpu_reps):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() > budget:
+            break
     torch.set_num_threads(prev)
-    best = min(timed, key=lambda k: timed[k][0])
-    t, reps = timed[best]
+    t = sorted(times)[len(times) // 2]
+    samples = B * args.frames * args.block_size
     return {"value": samples / t, "unit": "samples/s", "cores": best, "kind": "port",
             "host_cpu_count": host, "affinity_cpus": affinity,
-            "by_threads": {str(k): round(samples / v[0], 1) for k, v in timed.items()},
+            "by_threads": {str(k): round(v, 1) for k, v in sorted(by_threads.items())},
             "sample": f"oracle/torch_ref.synth_path (reference ATen op sequence), batch {B} of "
                       f"config {args.config} (F={args.frames}, bs={args.block_size}, H={args.harmonics}, "
-                      f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {reps} runs, "
-                      f"{t:.3f} s each at {best} threads (faster of {sorted(timed)} threads; host "
-                      f"os.cpu_count() = {host})"}
+                      f"NB={args.bands}, {args.reverb_length}-tap reverb), median of {len(times)} runs, "
+                      f"{t:.3f} s each at {best} threads (the fastest of the by_threads sweep, timed on "
+                      f"{sweep_b} items; host os.cpu_count() = {host})"}
 
 
 def train_leg(args, inp, dev, reps=20):
@@ -356,6 +381,38 @@ def decoder_leg(args, inp, dev, reps=10):
                      f"{args.reverb_length}), random init, batch {B} x {F} frames"}
 
 
+def decoder_synthesis_leg(args, inp, dev, reps=50):
+    """The synthesis section of DDSPDecoder.forward (decoder.py:106-125: the two projections, both
+    synths with their controls, the sum, the returned parts and control dicts, the 1 s reverb) as the
+    decoder runs it (decoder.decoder_synthesize, the fused kernel; install() binds the same function
+    under the reference's DDSPDecoder.forward), from a fixed GRU output; device noise."""
+    from ddsp_pytorch_amd.decoder import DDSPDecoder, decoder_synthesize
+    B, F, bs = args.batch, args.frames, args.block_size
+    torch.manual_seed(0)
+    model = DDSPDecoder(512, args.harmonics, args.bands, args.sample_rate, bs, True).to(dev).eval()
+    model.noise_synth.noise_mode = "device"
+    if args.reverb_length != args.sample_rate:
+        model.reverb = type(model.reverb)(args.reverb_length, args.sample_rate).to(dev)
+    with torch.no_grad():
+        hidden = model.decoder(inp["f0"], torch.randn(B, F, 1, device=dev))
+        run = lambda: decoder_synthesize(model, hidden, inp["f0"])
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = run()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+    assert torch.isfinite(out[0]).all()
+    del model
+    return {"value": round(B * F * bs / t, 1), "unit": "samples/s", "ms_per_step": round(t * 1e3, 4),
+            "workload": f"decoder.py:106-125 synthesis section of DDSPDecoder(hidden 512, H {args.harmonics}, "
+                        f"NB {args.bands}, reverb {args.reverb_length}) from a fixed GRU output: projections, "
+                        "fused synthesis writing signal + harmonic + noise + control dicts, reverb; batch "
+                        f"{B} x {F} frames, device noise"}
+
+
 def _sync(dev):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -464,7 +521,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # launched by torch.distributed.run (WORLD_SIZE set, 1 included): one process per GPU over RCCL
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -545,19 +603,31 @@ def main():
     n_sin = B * F * bs * H
     osc_slots = n_sin / 64 * OSC_SLOTS_PER_SINE
     vc = load_traffic(args.valu_counts).get(f"config{args.config}", {})
-    if vc.get("SQ_INSTS_VALU"):
+    src_sha = kernel_source_sha()
+    stale = bool(vc) and vc.get("source_sha") != src_sha
+    if vc.get("SQ_INSTS_VALU") and not stale:
         slots = vc["SQ_INSTS_VALU"] + (SIN_SLOTS - 1) * n_sin / 64
         slots_src = (f"PMC SQ_INSTS_VALU {vc['SQ_INSTS_VALU']:.4g} wave-instructions per launch "
                      f"({args.valu_counts.replace(ROOT + os.sep, '')}) + {SIN_SLOTS - 1} extra slots per "
                      "v_sin_f32 wave-instruction")
     else:
         slots = osc_slots
-        slots_src = "oscillator model only (no PMC counts for this configuration)"
+        slots_src = ("oscillator model only (" + ("the PMC counts were taken on other kernel sources"
+                     if stale else "no PMC counts for this configuration") + ")")
+    # algorithmic issue slots: per sample H x (6 VALU + v_sin_f32 at 4 slots) for the
+    # oscillator + 127 FIR taps (one FMA each) for the noise filter; no controls, RNG or addressing
+    fir_taps = 2 * (NB - 1) - 1
+    alg_slots = B * F * bs / 64 * (H * OSC_SLOTS_PER_SINE + fir_taps)
     achieved = slots / (osc_ms * 1e-3)
     osc_bytes = 4 * (H + 2) * B * F * bs
     roofline = {"bound": "valu", "achieved": round(achieved / 1e12, 4), "peak": VALU_PEAK_SLOTS / 1e12,
                 "unit": "T issue slots/s (wave64 VALU: fp32 op 1 slot = 2 SIMD cycles, v_sin_f32 4 slots)",
                 "frac": round(achieved / VALU_PEAK_SLOTS, 4),
+                "frac_algorithmic": round(alg_slots / (osc_ms * 1e-3) / VALU_PEAK_SLOTS, 4),
+                "algorithmic_slots_per_launch": round(alg_slots),
+                "algorithmic_slots_note": f"samples/64 x (H x {OSC_SLOTS_PER_SINE} + {fir_taps}): per (sample, "
+                                          "harmonic) 6 VALU + v_sin_f32 (4 slots), per sample the 127-tap noise FIR",
+                "valu_counts_source_sha": vc.get("source_sha"), "kernel_source_sha": src_sha,
                 "traffic": traffic.get("synth_frame_kernel"),
                 "kernel": "synth_frame_kernel (oscillator bank + filtered noise + their controls, fused)",
                 "avg_launch_ms": round(osc_ms, 4), "slots_per_launch": round(slots),
@@ -628,6 +698,11 @@ def main():
 
     if dist and not args.no_gather:
         r, g = gathered_leg(step, B * world, samples_per_step, args.steps, dev, dist)
+        if args.noise == "inject":  # deterministic: rank 0's shard of the gathered batch vs its own step
+            if rank == 0:
+                ref = step()
+                r["check_vs_local_step"] = {"equal": bool(torch.equal(g[:B], ref)),
+                                            "max_abs_diff": float((g[:B] - ref).abs().max())}
         result["gathered"] = r
         del g
         # root-held batch: controls scattered from rank 0 in chunks, audio gathered back,
@@ -641,6 +716,11 @@ def main():
             held = [full[k] for k in keys]
         r, g = scatter_gather_leg(syn, held, B * world, tails, samples_per_step, args.steps, args.chunks,
                                   dev, dist, reverb=syn.reverb)
+        if args.noise == "inject" and rank == 0:  # the gathered batch vs one process synthesising it all
+            with torch.no_grad():
+                ref = syn(*held)
+            r["check_vs_one_process_step"] = {"equal": bool(torch.equal(g, ref)),
+                                              "max_abs_diff": float((g - ref).abs().max())}
         result["scatter_gather"] = r
         del g, held
 
@@ -675,6 +755,7 @@ def main():
 
     if rank == 0 and not args.no_decoder_leg:
         result["decoder_forward"] = decoder_leg(args, inp, dev)
+        result["decoder_synthesis"] = decoder_synthesis_leg(args, inp, dev)
 
     if rank == 0 and not args.no_model_train_leg:
         result["model_train_step"] = model_train_leg(args, inp, dev)

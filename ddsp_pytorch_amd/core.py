@@ -360,13 +360,18 @@ def synth_frames_in_envelope(n_harmonic, n_bands, block_size, batch=1):
     return 4 * floats <= 120 * 1024
 
 
-def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None, parts=False):
+def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None, parts=False, controls=False):
     """decoder.py:106-121 in one kernel: raw harmonic projection param[B,F,H+1], pitch f0[B,F,1]
     and raw noise projection mags[B,F,NB] -> signal = harmonic + noise [B,F*bs,1].
 
     ``noise`` [B,F,bs] injects the U[-1,1) samples (else on-device Philox).  With ``parts`` the
-    harmonic and noise signals are returned too.  Returns None when the shape is outside the
-    fused kernel's envelope (block_size % 4 == 0 and <= 1024, H <= 1024, NB <= 1025)."""
+    harmonic and noise signals are returned too: (signal, harmonic, noise).  With ``controls``
+    the controls ``DDSPDecoder.forward`` returns (decoder.py:127-135) are appended as a dict
+    ``{"amplitudes" [B,F,1], "harmonic_distribution" [B,F,H], "magnitudes" [B,F,NB]}`` — the
+    distribution as the reference's caller sees it after ``modules.py:73``'s in-place
+    ``*= amplitudes``; written by the same launch (or, under autograd, by the differentiable
+    control ops).  Returns None when the shape is outside the fused kernel's envelope
+    (block_size % 4 == 0 and <= 1024, H <= 1024, NB <= 1025)."""
     _dev(f0, param, mags)
     B, F, H1 = param.shape
     NB = mags.shape[-1]
@@ -377,12 +382,20 @@ def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None
         return None
     if _wants_grad(f0, param, mags):
         _grad.refuse_f0_grad(f0, "synth_frames")
-        return _grad.SynthFramesFn.apply(f0, param, mags, bs, float(sample_rate), float(bias), noise, bool(parts))
+        outs = _grad.SynthFramesFn.apply(f0, param, mags, bs, float(sample_rate), float(bias), noise,
+                                         bool(parts))
+        if not controls:
+            return outs
+        amps, dist = harmonic_controls(param[..., :1], param[..., 1:], f0, sample_rate)
+        ctrl = {"amplitudes": amps, "harmonic_distribution": dist * amps,
+                "magnitudes": scale_with_bias(mags, bias)}
+        return (*outs, ctrl) if parts else (outs, ctrl)
     seed, offset = _noise_counter.next() if noise is None else (0, 0)
-    return _synth_frames_launch(f0, param, mags, bs, sample_rate, bias, noise, parts, seed, offset)
+    return _synth_frames_launch(f0, param, mags, bs, sample_rate, bias, noise, parts, seed, offset, controls)
 
 
-def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, parts, seed, offset):
+def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, parts, seed, offset,
+                         controls=False):
     B, F, H1 = param.shape
     NB = mags.shape[-1]
     bs = int(block_size)
@@ -395,10 +408,18 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     out = torch.empty(B, F * bs, 1, dtype=torch.float32, device=f0.device)
     harm = torch.empty_like(out) if parts else None
     nz = torch.empty_like(out) if parts else None
-    _lib.call("synth_frames", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
-              seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), B, F, H1 - 1, NB, bs,
+    ctrl = (torch.empty(B * F * (1 + (H1 - 1) + NB), dtype=torch.float32, device=f0.device)
+            if controls else None)
+    _lib.call("synth_frames_controls", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
+              seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), _lib.ptr(ctrl), B, F, H1 - 1, NB, bs,
               float(sample_rate), _lib.stream_of(out))
-    return (out, harm, nz) if parts else out
+    res = (out, harm, nz) if parts else out
+    if not controls:
+        return res
+    BF, H = B * F, H1 - 1
+    cd = {"amplitudes": ctrl[:BF].view(B, F, 1), "harmonic_distribution": ctrl[BF:BF * (1 + H)].view(B, F, H),
+          "magnitudes": ctrl[BF * (1 + H):].view(B, F, NB)}
+    return (*res, cd) if parts else (res, cd)
 
 
 def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed, bias=-5.0):

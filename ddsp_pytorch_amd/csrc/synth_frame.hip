@@ -29,14 +29,16 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // at wave w0 of the workgroup) in the LDS region smem4; every wave of the workgroup calls it (its
 // barriers are workgroup barriers).  On return (true: the thread's samples j0..j0+3 are in the
 // frame) acc = harmonic, nz = filtered noise.
-// PAD: one s_nop ahead of the sine loop (code placement, see phase 5)
-template <bool RNG, bool SPLIT, bool PAD>
+// PAD: one s_nop ahead of the (non-SPLIT) sine loop where an instantiation needs it for the loop's fast
+// placement (phase 5; the controls-writing instantiations).  CTRL: also write the frame's controls
+// (the dicts DDSPDecoder.forward returns) to ctrl_out.
+template <bool RNG, bool SPLIT, bool PAD, bool CTRL>
 __device__ __forceinline__ bool frame_synth(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
-    const uint64_t* __restrict__ counter, int F, int H, int NB, int bs, float sr, int lo_end, int tail_start,
-    int pad, int f, int b, int tid, int NT, float4* smem4, double* red, int w0, float (&acc)[4],
-    float (&nz)[4], int& j0_out) {
+    const uint64_t* __restrict__ counter, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs,
+    float sr, int lo_end, int tail_start, int pad, int f, int b, int tid, int NT, float4* smem4, double* red,
+    int w0, float (&acc)[4], float (&nz)[4], int& j0_out) {
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
   float2* coef = reinterpret_cast<float2*>(smem4);       // [H4] (k+1, amplitude)
@@ -212,6 +214,19 @@ __device__ __forceinline__ bool frame_synth(
       acc[3] = h4.w;
     }
   }
+  // the controls the reference returns (decoder.py:127-135), when asked for, from LDS after the sine loop
+  // (registers are free here): ctrl_out = [amplitudes B*F | harmonic_distribution after modules.py:73's
+  // in-place `*= amplitudes`, B*F*H | magnitudes B*F*NB]
+  if constexpr (CTRL) {
+    // (the empty asm re-defines the base here, so no address of these stores is hoisted above the sine
+    // loop, where it would hold registers through it)
+    float* co = ctrl_out;
+    asm volatile("" : "+s"(co));
+    const int64_t BF = (int64_t)B * F;
+    if (tid == 0) co[frame] = scale_fn(prow[0]);
+    for (int k = tid; k < H; k += NT) co[BF + frame * H + k] = coef[k].y;
+    for (int k = tid; k < NB; k += NT) co[BF * (1 + H) + frame * NB + k] = A[k];
+  }
   if (!active) return false;
 
   // ---- phase 6: filtered noise for the same samples ----
@@ -230,20 +245,20 @@ __device__ __forceinline__ bool frame_synth(
   return true;
 }
 
-template <bool RNG, bool SPLIT>
+template <bool RNG, bool SPLIT, bool CTRL>
 __global__ void __launch_bounds__(256) synth_frame_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
-    float* __restrict__ noise_out, int F, int H,
+    float* __restrict__ noise_out, float* __restrict__ ctrl_out, int F, int H,
     int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
   extern __shared__ float4 smem4[];
   __shared__ double red[32];
   float acc[4], nz[4];
   int j0;
-  if (!frame_synth<RNG, SPLIT, SPLIT>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, F, H, NB, bs, sr, lo_end,
-                               tail_start, pad, blockIdx.x, blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc,
-                               nz, j0))
+  if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
+                                      (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
+                                      blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0))
     return;
   const int64_t o = ((int64_t)blockIdx.y * F + blockIdx.x) * bs + j0;
   if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -263,7 +278,7 @@ extern "C" {
 
 static int synth_frames_launch(const float* f0, const float* param, const float* raw_magnitudes, float bias,
                                const float* noise, uint64_t seed, uint64_t offset, uint64_t* counter, float* out,
-                               float* harmonic_out, float* noise_out, int64_t batch, int64_t frames,
+                               float* harmonic_out, float* noise_out, float* controls_out, int64_t batch, int64_t frames,
                                int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                                void* stream) {
   if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
@@ -300,10 +315,15 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
   const dim3 grid((unsigned)frames, (unsigned)batch), block((unsigned)(nt * G));
 #define DDSP_SYNTH_FRAME_LAUNCH(RNG_, SPLIT_)                                                              \
-  hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
+  do {                                                                                                  \
+    if (controls_out) DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, true);                                       \
+    else DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, false);                                                  \
+  } while (0)
+#define DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, CTRL_)                                                      \
+  hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_, CTRL_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
                      bias, RNG_ ? nullptr : noise, k0, k1, o0, o1, RNG_ ? counter : nullptr, out, harmonic_out,  \
-                     noise_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, \
-                     pad)
+                     noise_out, controls_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, \
+                     tail_start, pad)
   if (noise) {
     if (G > 1) DDSP_SYNTH_FRAME_LAUNCH(false, true);
     else DDSP_SYNTH_FRAME_LAUNCH(false, false);
@@ -312,6 +332,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
     else DDSP_SYNTH_FRAME_LAUNCH(true, false);
   }
 #undef DDSP_SYNTH_FRAME_LAUNCH
+#undef DDSP_SYNTH_FRAME_LAUNCH_
   if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
   return launch_status();
 }
@@ -322,7 +343,17 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                           int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                           void* stream) {
   return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
-                             noise_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
+                             noise_out, nullptr, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
+}
+
+int ddsp_hip_synth_frames_controls(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                   const float* noise, uint64_t seed, uint64_t offset, float* out,
+                                   float* harmonic_out, float* noise_out, float* controls_out, int64_t batch,
+                                   int64_t frames, int64_t n_harmonic, int64_t n_bands, int64_t block_size,
+                                   float sample_rate, void* stream) {
+  return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
+                             noise_out, controls_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate,
+                             stream);
 }
 
 int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const float* raw_magnitudes, float bias,
@@ -331,7 +362,7 @@ int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const flo
                                   void* stream) {
   if (!counter) return DDSP_HIP_EINVAL;
   return synth_frames_launch(f0, param, raw_magnitudes, bias, nullptr, seed, 0, counter, out, nullptr, nullptr,
-                             batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
+                             nullptr, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
 }
 
 }  // extern "C"

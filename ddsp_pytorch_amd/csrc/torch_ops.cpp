@@ -226,6 +226,62 @@ at::Tensor filtered_noise(const at::Tensor& magnitudes, int64_t block_size, cons
   return out;
 }
 
+// decoder.py:106-121 in one launch (ddsp_hip_synth_frames): harmonic + filtered noise, their controls and
+// the sum; outside the fused kernel's shape envelope the two module kernels (harmonic_synth_params, then
+// filtered_noise adding the harmonic).  parts: the harmonic and noise signals as well.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> synth_frames_impl(const at::Tensor& f0, const at::Tensor& param,
+                                                                 const at::Tensor& mags, int64_t block_size,
+                                                                 double sample_rate, double bias,
+                                                                 const std::optional<at::Tensor>& noise,
+                                                                 int64_t seed, int64_t offset, bool parts) {
+  check_dev(f0, "f0");
+  check_dev(param, "param");
+  check_dev(mags, "mags");
+  TORCH_CHECK(param.dim() == 3 && mags.dim() == 3, "synth_frames: param [B,F,H+1] and mags [B,F,NB] expected");
+  const int64_t B = param.size(0), F = param.size(1), H1 = param.size(2), NB = mags.size(2);
+  TORCH_CHECK(f0.sizes() == at::IntArrayRef({B, F, 1}) && mags.size(0) == B && mags.size(1) == F && H1 >= 2,
+              "synth_frames: f0 [B,F,1], param [B,F,H+1], mags [B,F,NB] expected");
+  at::Tensor f = c16(f0), p = c16(param), m = c16(mags), n;
+  if (noise.has_value()) {
+    check_dev(*noise, "noise");
+    TORCH_CHECK(noise->sizes() == at::IntArrayRef({B, F, block_size}), "synth_frames: noise must be [B,F,bs]");
+    n = c16(*noise);
+  }
+  const float* np = n.defined() ? n.data_ptr<float>() : nullptr;
+  at::Tensor out = at::empty({B, F * block_size, 1}, f.options());
+  at::Tensor harm = parts ? at::empty_like(out) : at::Tensor();
+  at::Tensor nz = parts ? at::empty_like(out) : at::Tensor();
+  int st = ddsp_hip_synth_frames(f.data_ptr<float>(), p.data_ptr<float>(), m.data_ptr<float>(), (float)bias, np,
+                                 (uint64_t)seed, (uint64_t)offset, out.data_ptr<float>(),
+                                 parts ? harm.data_ptr<float>() : nullptr, parts ? nz.data_ptr<float>() : nullptr, B,
+                                 F, H1 - 1, NB, block_size, (float)sample_rate, stream_of(f));
+  if (st == DDSP_HIP_ERANGE) {  // outside the fused kernel's envelope: the two module kernels
+    at::Tensor h = parts ? harm : at::empty_like(out);
+    ok(ddsp_hip_harmonic_synth_params(f.data_ptr<float>(), p.data_ptr<float>(), h.data_ptr<float>(), B, F, H1 - 1,
+                                      block_size, (float)sample_rate, stream_of(f)),
+       "harmonic_synth_params");
+    st = ddsp_hip_filtered_noise_params(m.data_ptr<float>(), (float)bias, np, (uint64_t)seed, (uint64_t)offset,
+                                        h.data_ptr<float>(), out.data_ptr<float>(),
+                                        parts ? nz.data_ptr<float>() : nullptr, B, F, NB, block_size, stream_of(f));
+  }
+  ok(st, "synth_frames");
+  return {out, harm, nz};
+}
+
+at::Tensor synth_frames(const at::Tensor& f0, const at::Tensor& param, const at::Tensor& mags, int64_t block_size,
+                        double sample_rate, double bias, const std::optional<at::Tensor>& noise, int64_t seed,
+                        int64_t offset) {
+  return std::get<0>(synth_frames_impl(f0, param, mags, block_size, sample_rate, bias, noise, seed, offset, false));
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> synth_frames_parts(const at::Tensor& f0, const at::Tensor& param,
+                                                                  const at::Tensor& mags, int64_t block_size,
+                                                                  double sample_rate, double bias,
+                                                                  const std::optional<at::Tensor>& noise,
+                                                                  int64_t seed, int64_t offset) {
+  return synth_frames_impl(f0, param, mags, block_size, sample_rate, bias, noise, seed, offset, true);
+}
+
 at::Tensor reverb_build_impulse(const at::Tensor& noise, const at::Tensor& decay, const at::Tensor& wet,
                                 double sample_rate) {
   check_dev(noise, "noise");  // modules.py:21-26
@@ -306,6 +362,10 @@ TORCH_LIBRARY(ddsp_hip, m) {
   m.def("harmonic_synth_params(Tensor f0, Tensor param, int block_size, float sample_rate) -> Tensor");
   m.def("filtered_noise(Tensor magnitudes, int block_size, Tensor? noise=None, int seed=0, int offset=0,"
         " Tensor? add=None, float? raw_bias=None) -> Tensor");
+  m.def("synth_frames(Tensor f0, Tensor param, Tensor mags, int block_size, float sample_rate, float bias=-5.0,"
+        " Tensor? noise=None, int seed=0, int offset=0) -> Tensor");
+  m.def("synth_frames_parts(Tensor f0, Tensor param, Tensor mags, int block_size, float sample_rate,"
+        " float bias=-5.0, Tensor? noise=None, int seed=0, int offset=0) -> (Tensor, Tensor, Tensor)");
   m.def("reverb_build_impulse(Tensor noise, Tensor decay, Tensor wet, float sample_rate) -> Tensor");
   m.def("reverb_spectrum(Tensor impulse, int n_samples) -> Tensor");
   m.def("reverb_apply(Tensor x, Tensor spectrum, int ir_length) -> Tensor");
@@ -323,6 +383,8 @@ TORCH_LIBRARY_IMPL(ddsp_hip, CUDA, m) {  // HIP tensors dispatch under the CUDA 
   m.impl("harmonic_synth_frames", &harmonic_synth_frames);
   m.impl("harmonic_synth_params", &harmonic_synth_params);
   m.impl("filtered_noise", &filtered_noise);
+  m.impl("synth_frames", &synth_frames);
+  m.impl("synth_frames_parts", &synth_frames_parts);
   m.impl("reverb_build_impulse", &reverb_build_impulse);
   m.impl("reverb_spectrum", &reverb_spectrum);
   m.impl("reverb_apply", &reverb_apply);

@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 
 from . import core
-from .modules import FilteredNoise, HarmonicSynth, Reverb
+from .modules import NOISE_MODES, FilteredNoise, HarmonicSynth, Reverb
 
 
 def mlp(in_size, hidden_size, n_layers):
@@ -62,6 +62,52 @@ def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
     return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
 
 
+def decoder_synthesize(self, hidden, f0):
+    """decoder.py:106-125, the synthesis section of DDSPDecoder.forward: controls -> harmonic + noise
+    (+ reverb).  On the fused kernel (one launch for both synths, their controls, the sum and the
+    returned control dicts) whenever the shapes are in its envelope: the reference's noise stream
+    (``noise_mode = "torch"``: torch.rand(B, F, bs) drawn as modules.py:119-123 draws it, injected)
+    or on-device Philox (``"device"``).  Outside the envelope the modules run one by one (still on the
+    gfx950 kernels).  Works on this package's DDSPDecoder and, through install(), on the reference's.
+    Returns (signal, harmonic, noise, harmonic_ctrls, noise_ctrls)."""
+    hs, ns = self.harmonic_synth, self.noise_synth
+    param = self.harmonic_proj(hidden)
+    mags = self.noise_proj(hidden)
+    H, NB, bs = param.shape[-1] - 1, mags.shape[-1], int(hs.block_size)
+    fused = (param.is_cuda and int(ns.block_size) == bs and param.shape[0] <= 65535
+             and core.synth_frames_in_envelope(H, NB, bs, param.shape[0]))
+    if fused:
+        mode = getattr(ns, "noise_mode", "torch")
+        if mode not in NOISE_MODES:
+            raise ValueError(f"noise_mode must be one of {NOISE_MODES}")
+        noise_in = FilteredNoise.draw_noise(ns, mags) if mode == "torch" else None
+        signal, harmonic, noise, ctrl = core.synth_frames(
+            f0, param, mags, bs, hs.sample_rate, bias=float(ns.initial_bias), noise=noise_in, parts=True,
+            controls=True)
+        harmonic_ctrls = {"f0": f0, "harmonic_distribution": ctrl["harmonic_distribution"],
+                          "amplitudes": ctrl["amplitudes"]}
+        noise_ctrls = {"magnitudes": ctrl["magnitudes"]}
+    else:
+        harmonic_ctrls = hs.get_controls(param[..., :1], param[..., 1:], f0)
+        harmonic = hs(**harmonic_ctrls)
+        noise_ctrls = ns.get_controls(mags)
+        noise = ns(**noise_ctrls)
+        signal = harmonic + noise
+    if self.has_reverb:
+        signal = self.reverb(signal)
+    return signal, harmonic, noise, harmonic_ctrls, noise_ctrls
+
+
+def decoder_forward(self, batch: dict):
+    """decoder.py:101-136 DDSPDecoder.forward with the synthesis section fused (decoder_synthesize);
+    install() binds it to the reference's DDSPDecoder."""
+    f0, loudness = batch["pitch"], batch["loudness"]
+    hidden = self.decoder(f0, loudness)
+    signal, harmonic, noise, hc, nc = decoder_synthesize(self, hidden, f0)
+    return {"f0": f0, "loudness": loudness, "signal": signal, "noise": noise,
+            "harmonic_audio": harmonic, "noise_ctrls": nc, "harmonic_ctrls": hc}
+
+
 class DDSPDecoder(nn.Module):
     """ddsp/models/decoder.py:70-136 with the synthesis on gfx950 kernels."""
 
@@ -79,21 +125,5 @@ class DDSPDecoder(nn.Module):
         self.reverb = Reverb(sample_rate, sample_rate)
         self.register_buffer("phase", torch.zeros(1))
 
-    def synthesize(self, hidden, f0):
-        """decoder.py:106-125: controls -> harmonic + noise (+ reverb)."""
-        param = self.harmonic_proj(hidden)
-        harmonic_ctrls = self.harmonic_synth.get_controls(param[..., :1], param[..., 1:], f0)
-        harmonic = self.harmonic_synth(**harmonic_ctrls)
-        noise_ctrls = self.noise_synth.get_controls(self.noise_proj(hidden))
-        noise = self.noise_synth(**noise_ctrls)
-        signal = harmonic + noise
-        if self.has_reverb:
-            signal = self.reverb(signal)
-        return signal, harmonic, noise, harmonic_ctrls, noise_ctrls
-
-    def forward(self, batch: dict):
-        f0, loudness = batch["pitch"], batch["loudness"]
-        hidden = self.decoder(f0, loudness)
-        signal, harmonic, noise, hc, nc = self.synthesize(hidden, f0)
-        return {"f0": f0, "loudness": loudness, "signal": signal, "noise": noise,
-                "harmonic_audio": harmonic, "noise_ctrls": nc, "harmonic_ctrls": hc}
+    synthesize = decoder_synthesize
+    forward = decoder_forward

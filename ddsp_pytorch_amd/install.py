@@ -63,9 +63,13 @@ def install(pkg=None, functions=True, module_forwards=True):
             for name in names:
                 saved_methods[(ref_cls, name)] = ref_cls.__dict__.get(name)
                 setattr(ref_cls, name, ours.__dict__[name])
-        # the decoder network's GRU recurrence (decoder.py:43-68) on the step kernel
-        ref_dec = getattr(getattr(pkg.models, "decoder", None), "GRUDecoder", None)
-        if ref_dec is not None:
-            saved_methods[(ref_dec, "forward")] = ref_dec.__dict__.get("forward")
-            setattr(ref_dec, "forward", decoder.gru_decoder_forward)
+        # the decoder network's GRU recurrence (decoder.py:43-68) on the step kernel, and
+        # DDSPDecoder.forward (decoder.py:101-136) with its synthesis section on the fused kernel
+        # (both synths, their controls, the sum and the returned control dicts in one launch)
+        ref_decoder_mod = getattr(pkg.models, "decoder", None)
+        for cls_name, fn in (("GRUDecoder", decoder.gru_decoder_forward), ("DDSPDecoder", decoder.decoder_forward)):
+            ref_cls = getattr(ref_decoder_mod, cls_name, None)
+            if ref_cls is not None:
+                saved_methods[(ref_cls, "forward")] = ref_cls.__dict__.get("forward")
+                setattr(ref_cls, "forward", fn)
     return Installation(pkg, saved_fns, saved_methods)

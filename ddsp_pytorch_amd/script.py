@@ -101,19 +101,19 @@ class ScriptDecoder(nn.Module):
         self.noise_calls = 0
 
     def synthesize(self, f0: torch.Tensor, hidden: torch.Tensor, with_reverb: bool) -> torch.Tensor:
-        # decoder.py:106-125: harmonic (get_controls + forward fused) + noise (fused, adds
-        # the harmonic signal) + reverb
+        # decoder.py:106-125: both synths, their controls and the sum in one launch
+        # (torch.ops.ddsp_hip.synth_frames, the fused kernel), then the reverb
         param = self.harmonic_proj(hidden)
-        harmonic = torch.ops.ddsp_hip.harmonic_synth_params(f0, param, self.bs, self.sr)
         mags = self.noise_proj(hidden)
         B, F = mags.shape[0], mags.shape[1]
         if self.device_noise:
             self.noise_calls += 1
-            signal = torch.ops.ddsp_hip.filtered_noise(mags, self.bs, None, 0x5EEDDD5B, self.noise_calls,
-                                                       harmonic, self.initial_bias)
+            signal = torch.ops.ddsp_hip.synth_frames(f0, param, mags, self.bs, self.sr, self.initial_bias, None,
+                                                     0x5EEDDD5B, self.noise_calls)
         else:
             noise = (torch.rand(B, F, self.bs) * 2 - 1).to(mags)  # modules.py:119-123
-            signal = torch.ops.ddsp_hip.filtered_noise(mags, self.bs, noise, 0, 0, harmonic, self.initial_bias)
+            signal = torch.ops.ddsp_hip.synth_frames(f0, param, mags, self.bs, self.sr, self.initial_bias, noise, 0,
+                                                     0)
         if with_reverb:
             signal = self.reverb(signal)
         return signal

@@ -117,14 +117,24 @@ class PipelinedSynthPath:
         on_default = cur == torch.cuda.default_stream(cur.device)
         if not on_default:
             self.s_synth.wait_stream(cur)  # inputs written on the caller's stream
+            # ... and not handed to the caller's stream's next allocations (the caller may drop them as
+            # soon as this returns) before the synthesis stream has read them
+            for t in (f0, param, mags, noise):
+                if t is not None:
+                    t.record_stream(self.s_synth)
         with torch.cuda.stream(self.s_synth):
             signal = self.path.synthesize(f0, param, mags, noise)
             done = torch.cuda.Event()
             done.record(self.s_synth)
+        rv = self.path.reverb
         with torch.cuda.stream(self.s_reverb):
             self.s_reverb.wait_event(done)
             signal.record_stream(self.s_reverb)  # its memory is not reused before the reverb read it
-            out = self.path.reverb(signal)
+            # the IR spectrum the reverb reads: cached by the module, possibly allocated on another stream
+            # and freed by a later invalidate() / parameter change while this stream still reads it
+            spec = rv._spectrum(signal.shape[1])
+            spec.record_stream(self.s_reverb)
+            out = core.reverb_apply(signal, spec, rv.length)
         if not on_default:
             out.record_stream(cur)
         return out
@@ -150,9 +160,10 @@ class SynthGraph:
       (``ddsp_hip_synth_frames_counter``), advanced on the stream by every replay — replay k draws
       the noise of ``core.synth_frames`` at offset k (parity: tests/test_gpu_device_noise.py).
     * ``rebuild_ir=True`` also captures ``Reverb.build_impulse`` and the IR spectrum
-      (modules.py:30-33 rebuilds them on every forward); by default the spectrum cached by the
-      module (``Reverb._spectrum``) is captured, so re-capture after changing the reverb's
-      parameters.
+      (modules.py:30-33 rebuilds them on every forward); by default the spectrum of the reverb's
+      parameters at capture time is copied into a buffer the graph owns (the module's cached
+      spectrum may be freed and its memory reused by invalidate() or a forward of another length),
+      so re-capture after changing the reverb's parameters.
     """
 
     def __init__(self, path, f0, param, mags, noise=None, seed=0x5EEDDD5B, rebuild_ir=False, warmup=2):
@@ -163,6 +174,10 @@ class SynthGraph:
         self.seed = int(seed)
         self.rebuild_ir = bool(rebuild_ir)
         self.counter = torch.zeros(1, dtype=torch.int64, device=f0.device)
+        self.spec = None
+        if path.reverb is not None and not self.rebuild_ir:
+            with torch.no_grad():
+                self.spec = path.reverb._spectrum(f0.shape[1] * path.block_size).clone()
         if noise is None and not core.synth_frames_in_envelope(param.shape[-1] - 1, mags.shape[-1],
                                                                path.block_size, param.shape[0]):
             raise RuntimeError("SynthGraph: device noise needs the fused kernel's shape envelope")
@@ -195,7 +210,7 @@ class SynthGraph:
         if self.rebuild_ir:
             spec = core.reverb_spectrum(rv.build_impulse(), sig.shape[1])
         else:
-            spec = rv._spectrum(sig.shape[1])
+            spec = self.spec  # owned by the graph
         return core.reverb_apply(sig, spec, rv.length)
 
     def reset(self):

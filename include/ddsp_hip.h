@@ -140,6 +140,18 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                           int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                           void* stream);
 
+/* ddsp_hip_synth_frames that also writes the controls DDSPDecoder.forward returns
+ * (decoder.py:127-135: output['harmonic_ctrls'], output['noise_ctrls']) into controls_out (nullable),
+ * laid out as [amplitudes B*F | harmonic_distribution B*F*H | magnitudes B*F*NB]: amplitudes =
+ * scale_function(param[...,0]), harmonic_distribution = the normalised distribution after
+ * HarmonicSynth.forward's in-place `*= amplitudes` (modules.py:61,73), magnitudes =
+ * scale_function(raw_magnitudes + bias) (modules.py:111-114). */
+int ddsp_hip_synth_frames_controls(const float* f0, const float* param, const float* raw_magnitudes, float bias,
+                                   const float* noise, uint64_t seed, uint64_t offset, float* out,
+                                   float* harmonic_out, float* noise_out, float* controls_out, int64_t batch,
+                                   int64_t frames, int64_t n_harmonic, int64_t n_bands, int64_t block_size,
+                                   float sample_rate, void* stream);
+
 /* ddsp_hip_synth_frames for a stream of calls replayed from a captured HIP graph (the ddsp~
  * realtime host, realtime/ddsp_tilde/ddsp_model.cpp:32-52, calling the exported model once per
  * 1024-sample buffer): the Philox offset of the on-device noise is read from the device word

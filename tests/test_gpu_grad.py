@@ -227,7 +227,11 @@ def test_reverb_grad_golden(dd, tag):
         assert relerr(t.grad, g[name]) < GRAD_REL, (name, relerr(t.grad, g[name]))
 
 
-@pytest.mark.parametrize("B,T,L", [(3, 102400, 48000), (2, 30000, 96000), (1, 2048, 2048)])
+# (2, 102400, 96000): config 4's 48 kernel windows, more than one round of the adjoint MAC's
+# 27-slot register ring; (1, 131072, 120000): 60 windows, three rounds, and the IR correlation's
+# 25-lag kernel over three lag blocks
+@pytest.mark.parametrize("B,T,L", [(3, 102400, 48000), (2, 30000, 96000), (1, 2048, 2048),
+                                   (2, 102400, 96000), (1, 131072, 120000)])
 def test_reverb_grad_oracle(dd, B, T, L):
     g = torch.Generator().manual_seed(B * T + L)
     torch.manual_seed(1)

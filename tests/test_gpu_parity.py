@@ -5,6 +5,7 @@ are held to tighter bounds where the math allows (stated per test).
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F_
 
 from conftest import load_golden, rms
 from oracle import numpy_oracle as no
@@ -233,6 +234,50 @@ def test_decoder_golden(dd):
     for key in ("harmonic_audio", "noise", "signal"):
         e = rms(C(o[key]), g[key])
         assert e < PARITY_RMS, (key, e)
+    # the control dicts, written by the same fused launch (decoder.py:127-135): the distribution as the
+    # reference's caller sees it after modules.py:73's in-place `*= amplitudes`
+    np.testing.assert_allclose(C(o["harmonic_ctrls"]["amplitudes"]), g["amplitudes"], rtol=5e-5)
+    np.testing.assert_allclose(C(o["harmonic_ctrls"]["harmonic_distribution"]), g["distribution"], rtol=5e-5,
+                               atol=1e-10)
+    np.testing.assert_allclose(C(o["noise_ctrls"]["magnitudes"]), g["magnitudes"], rtol=5e-5)
+    assert o["harmonic_ctrls"]["f0"] is not None
+
+
+def test_synth_frames_controls_output(dd):
+    """core.synth_frames(controls=True): the controls the launch writes equal the module kernels'
+    (HarmonicSynth.get_controls + the in-place *= amplitudes, FilteredNoise.get_controls), and the
+    signal is bit-identical to the launch without them."""
+    B, F, H, NB, bs, sr = 3, 7, 20, 9, 64, 48000
+    inp = dd.synth.make_inputs(B, F, H, NB, bs, seed=4, device="cuda")
+    with torch.no_grad():
+        plain = dd.core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr, noise=inp["noise"])
+        sig, harm, nz, c = dd.core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr, noise=inp["noise"],
+                                                parts=True, controls=True)
+        amps, dist = dd.core.harmonic_controls(inp["param"][..., :1], inp["param"][..., 1:], inp["f0"], sr)
+        mags = dd.core.scale_with_bias(inp["mags"], -5.0)
+    assert torch.equal(sig, plain) and torch.equal(harm + nz, sig)
+    torch.testing.assert_close(c["amplitudes"], amps, rtol=1e-6, atol=0)
+    torch.testing.assert_close(c["harmonic_distribution"], dist * amps, rtol=2e-6, atol=1e-12)
+    torch.testing.assert_close(c["magnitudes"], mags, rtol=1e-6, atol=0)
+
+
+def test_decoder_outside_fused_envelope(dd):
+    """DDSPDecoder.forward with block_size % 4 != 0 (outside the fused kernel's envelope): the modules
+    run one by one and the result still matches the oracle's decoder synthesis."""
+    torch.manual_seed(0)
+    m = dd.DDSPDecoder(64, 12, 9, 48000, 102, False).cuda().eval()
+    f0 = torch.full((2, 6, 1), 180.0, device="cuda")
+    loud = torch.randn(2, 6, 1, device="cuda")
+    with torch.no_grad():
+        torch.manual_seed(7)
+        o = m({"pitch": f0, "loudness": loud})
+        hidden = m.decoder(f0, loud)
+    torch.manual_seed(7)
+    noise = torch.rand(2, 6, 102) * 2 - 1
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    sig_r, harm_r, nz_r = tr.decoder_synthesis(sd, f0.cpu(), hidden.cpu(), noise, 102, 48000)
+    assert rms(C(o["signal"]), sig_r.numpy()) < 1e-6
+    assert rms(C(o["harmonic_audio"]), harm_r.numpy()) < 1e-6
 
 
 def _reference_shaped_modules():
@@ -333,6 +378,66 @@ def test_install_into_reference_style_package(dd):
     finally:
         inst.uninstall()
     assert pkg.harmonic_synth is tr.harmonic_synth
+
+
+def test_install_decoder_forward_on_reference_shaped_instance(dd):
+    """install() swaps the reference's DDSPDecoder.forward (decoder.py:101-136) for the fused-synthesis
+    forward; on an instance carrying only the reference's attributes it reproduces the oracle's
+    decoder synthesis (reference RNG stream for the noise, 1 s reverb) and the control dicts."""
+    import types
+    import torch.nn as nn
+    mods = _reference_shaped_modules()
+
+    class DDSPDecoder(nn.Module):  # decoder.py:76-99: the constructor's fields only
+        def __init__(self, hidden_size, n_harmonic, n_bands, sample_rate, block_size, has_reverb):
+            super().__init__()
+            self.register_buffer("sample_rate", torch.tensor(sample_rate))
+            self.register_buffer("block_size", torch.tensor(block_size))
+            self.decoder = dd.decoder.GRUDecoder(hidden_size)
+            self.harmonic_proj = nn.Linear(hidden_size, n_harmonic + 1)
+            self.noise_proj = nn.Linear(hidden_size, n_bands)
+            self.harmonic_synth = mods.HarmonicSynth(block_size, sample_rate)
+            self.noise_synth = mods.FilteredNoise(block_size, n_bands)
+            self.has_reverb = has_reverb
+            self.reverb = mods.Reverb(sample_rate, sample_rate)
+            self.register_buffer("phase", torch.zeros(1))
+
+        def forward(self, batch):
+            raise AssertionError("install() should have replaced this")
+
+    pkg = types.ModuleType("ddsp_like")
+    for name in ("scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
+                 "amp_to_impulse_response", "fft_convolve"):
+        setattr(pkg, name, getattr(tr, name))
+    pkg.models = types.SimpleNamespace(modules=mods, decoder=types.SimpleNamespace(DDSPDecoder=DDSPDecoder))
+    B, F, H, NB, bs, sr = 2, 12, 24, 65, 256, 48000
+    torch.manual_seed(3)
+    model = DDSPDecoder(64, H, NB, sr, bs, True).cuda().eval()
+    f0 = (50.0 * 20.0 ** torch.rand(B, F, 1)).cuda()
+    loud = torch.randn(B, F, 1).cuda()
+    inst = dd.install(pkg)
+    try:
+        assert DDSPDecoder.forward is dd.decoder.decoder_forward
+        with torch.no_grad():
+            torch.manual_seed(123)
+            o = model({"pitch": f0, "loudness": loud})
+            hidden = model.decoder(f0, loud)
+    finally:
+        inst.uninstall()
+    assert DDSPDecoder.__dict__["forward"] is not dd.decoder.decoder_forward
+    torch.manual_seed(123)
+    noise = torch.rand(B, F, bs) * 2 - 1  # modules.py:119-123, the model's first draw in forward
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    rv = model.reverb
+    rv_r = tr.Reverb(rv.noise.detach().cpu(), rv.decay.detach().cpu(), rv.wet.detach().cpu(), sr, sr)
+    sig_r, harm_r, nz_r = tr.decoder_synthesis(sd, f0.cpu(), hidden.cpu(), noise, bs, sr, reverb=rv_r)
+    assert rms(C(o["harmonic_audio"]), harm_r.numpy()) < 1e-6
+    assert rms(C(o["noise"]), nz_r.numpy()) < 1e-6
+    assert rms(C(o["signal"]), sig_r.numpy()) < 2e-6 * max(1.0, float(sig_r.pow(2).mean().sqrt()))
+    param = F_.linear(hidden.cpu(), sd["harmonic_proj.weight"], sd["harmonic_proj.bias"])
+    amps_r, dist_r = tr.harmonic_controls(param[..., :1], param[..., 1:], f0.cpu(), sr)
+    np.testing.assert_allclose(C(o["harmonic_ctrls"]["harmonic_distribution"]), (dist_r * amps_r).numpy(),
+                               rtol=2e-5, atol=1e-10)
 
 
 # ------------------------------------------------------------------ full size (config 2)

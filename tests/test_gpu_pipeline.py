@@ -105,6 +105,18 @@ def test_pipelined_from_a_side_stream():
         got = [o.clone() for o in outs]
     torch.cuda.synchronize()
     assert all(torch.equal(g, r) for g, r in zip(got, ref))
+    # inputs dropped right after the call (temporaries): their blocks must not be handed to the side
+    # stream's next allocations, overwritten below, before the synthesis stream has read them
+    with torch.cuda.stream(side):
+        outs = []
+        for x in (a, b):
+            outs.append(pipe(*(x[k].clone() for k in ("f0", "param", "mags", "noise"))))
+            junk = [torch.full_like(x[k], 1e3) for k in ("f0", "param", "mags", "noise")]  # reuse attempt
+            del junk
+        pipe.join()
+        got = [o.clone() for o in outs]
+    torch.cuda.synchronize()
+    assert all(torch.equal(g, r) for g, r in zip(got, ref))
 
 
 
@@ -122,3 +134,26 @@ def test_pipelined_odd_shapes(B, F, H, NB, bs, L):
     torch.cuda.synchronize()
     for i, (o, r) in enumerate(zip(outs, ref)):
         assert o.shape == (B, F * bs, 1) and torch.equal(o, r), i
+
+
+def test_synth_graph_replays_and_owns_its_spectrum():
+    """synth.SynthGraph: replay k equals the eager step drawing device noise at offset k, and the graph
+    keeps reading the spectrum it captured after the module's cached spectrum was freed
+    (Reverb.invalidate) and its memory reused by an eager forward of another length."""
+    from ddsp_pytorch_amd import core
+    from ddsp_pytorch_amd.synth import SynthGraph, SynthPath, make_inputs
+    inp = make_inputs(4, 16, 24, 65, 512, seed=5, device="cuda", with_noise=False)
+    syn = SynthPath(512, 48000, reverb_length=48000).cuda()
+    g = SynthGraph(syn, inp["f0"], inp["param"], inp["mags"], seed=77)
+    r0, r1 = g.replay().clone(), g.replay().clone()
+    core.set_noise_seed(77)
+    with torch.no_grad():
+        e0 = syn(inp["f0"], inp["param"], inp["mags"])
+        e1 = syn(inp["f0"], inp["param"], inp["mags"])
+    assert torch.equal(r0, e0) and torch.equal(r1, e1) and not torch.equal(r0, r1)
+    syn.reverb.invalidate()
+    with torch.no_grad():
+        for n in (3, 5, 9):  # fresh spectra of other lengths, allocated where the old one lived
+            syn.reverb(torch.randn(2, n * 2048, 1, device="cuda"))
+    g.reset()
+    assert torch.equal(g.replay(), r0)

@@ -104,6 +104,7 @@ def test_install_resolves_on_reference_instances():
                  for c, names in install.METHODS.items() for n in names}
     orig_fns = {n: getattr(ddsp, n) for n in install.FUNCTIONS}
     orig_gru = ref_decoder.GRUDecoder.__dict__["forward"]
+    orig_dec = ref_decoder.DDSPDecoder.__dict__["forward"]
 
     inst = dd.install(ddsp)
     try:
@@ -125,6 +126,20 @@ def test_install_resolves_on_reference_instances():
         # reads behind `if getattr(self, "add_z", False)`: present on a reference instance with z
         with_z = ref_decoder.GRUDecoder(32, z_dim=4)
         assert guarded and all(hasattr(with_z, a) for a in guarded), guarded
+        # DDSPDecoder.forward with the fused synthesis section, against the reference's instance:
+        # every self.X it (and decoder_synthesize) reads exists on a reference DDSPDecoder, and the
+        # attributes it reads off the synth modules too
+        assert ref_decoder.DDSPDecoder.__dict__["forward"] is dd.decoder.decoder_forward
+        for fn in (dd.decoder.decoder_forward, dd.decoder.decoder_synthesize):
+            missing = {a for a in _self_reads(fn) if not hasattr(model, a)}
+            assert not missing, f"{fn.__name__} reads {missing}, absent on a reference DDSPDecoder"
+        for attr in ("block_size", "sample_rate"):
+            assert hasattr(model.harmonic_synth, attr)
+        for attr in ("block_size", "initial_bias"):
+            assert hasattr(model.noise_synth, attr)
+        batch = {"pitch": torch.full((1, 4, 1), 220.0), "loudness": torch.zeros(1, 4, 1)}
+        with pytest.raises(Exception):
+            model(batch)  # CPU tensors: the synthesis refuses (no CPU fallback)
         # the rebound functions: the same names, and no CPU fallback
         for n in install.FUNCTIONS:
             assert getattr(ddsp, n) is getattr(dd.core, n)
@@ -139,3 +154,4 @@ def test_install_resolves_on_reference_instances():
     for n, f in orig_fns.items():
         assert getattr(ddsp, n) is f
     assert ref_decoder.GRUDecoder.__dict__["forward"] is orig_gru
+    assert ref_decoder.DDSPDecoder.__dict__["forward"] is orig_dec

@@ -22,15 +22,17 @@ def test_script_compiles_and_calls_ops(tmp_path):
     m, _ = _model()
     s = script.export(m, str(tmp_path / "ddsp.ts"))
     graph = str(s.ddsp.synthesize.graph) + str(s.ddsp.reverb.graph)
-    for op in ("ddsp_hip::harmonic_synth_params", "ddsp_hip::filtered_noise", "ddsp_hip::reverb_apply"):
+    # the synthesis section is the fused kernel's operator (both synths, their controls, the sum)
+    for op in ("ddsp_hip::synth_frames", "ddsp_hip::reverb_apply"):
         assert op in graph, op
+    assert "ddsp_hip::filtered_noise" not in graph and "ddsp_hip::harmonic_synth_params" not in graph
     # reference state_dict layout under `ddsp.`
     ref_keys = set(m.state_dict())
     assert all("ddsp." + k in s.state_dict() for k in ref_keys)
     # round trip through the file
     script.load_ops()
     s2 = torch.jit.load(str(tmp_path / "ddsp.ts"))
-    assert "ddsp_hip::harmonic_synth_params" in str(s2.ddsp.synthesize.graph)
+    assert "ddsp_hip::synth_frames" in str(s2.ddsp.synthesize.graph)
 
 
 def test_scripted_ops_refuse_cpu_tensors():

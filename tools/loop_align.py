@@ -14,7 +14,7 @@ import sys
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-def analyze(so, kern="synth_frame_kernelILb1ELb0EE"):
+def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
     """the kernel's sine loop: start address, size, 8-byte instructions at odd dword addresses"""
     tmp = tempfile.mkdtemp()
     local = os.path.join(tmp, os.path.basename(so))
@@ -63,8 +63,9 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0EE"):
 
 # every shipped instantiation with a hardware-sine loop: fused forward (device noise / injected
 # noise, one sample per thread for few-frame launches), the harmonic-only fused backward
-SHIPPED = ("synth_frame_kernelILb1ELb0EE", "synth_frame_kernelILb0ELb0EE",
-           "synth_frame_kernelILb1ELb1EE", "synth_frame_kernelILb0ELb1EE",
+SHIPPED = ("synth_frame_kernelILb1ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0EE",
+           "synth_frame_kernelILb1ELb1ELb0EE", "synth_frame_kernelILb0ELb1ELb0EE",
+           "synth_frame_kernelILb1ELb0ELb1EE", "synth_frame_kernelILb0ELb0ELb1EE",
            "frame_backward_kernelILi2ELi2ELb1EE")
 
 
