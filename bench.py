@@ -44,19 +44,20 @@ SIN_SLOTS = 4
 OSC_SLOTS_PER_SINE = 6 + SIN_SLOTS         # per (sample, harmonic): 6 fp32 VALU ops + one v_sin_f32
                                            # (synth_frame.hip inner loop; tools/loop_align.py counts it)
 
-KERNEL_SOURCES = ("ddsp_pytorch_amd/csrc/synth_frame.hip", "ddsp_pytorch_amd/csrc/common.h",
-                  "ddsp_pytorch_amd/csrc/noise_dsp.h")
+DOMINANT_KERNEL = "synth_frame_kernelILb1ELb0ELb0EE"   # device noise, 4 samples/thread, no control dicts
 
 
 def kernel_source_sha():
-    """sha256 (16 hex) of the fused synthesis kernel's sources: PMC instruction counts recorded for
-    other sources (profiles/pmc_valu.json "source_sha") are stale and not used."""
-    import hashlib
-    h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    """sha256 (16 hex) of the dominant kernel's instruction stream in the built library
+    (tools/loop_align.kernel_sha): PMC instruction counts recorded for another build of that kernel
+    (profiles/pmc_valu.json "kernel_sha") are stale and not used."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import loop_align
+        from ddsp_pytorch_amd import _lib
+        return loop_align.kernel_sha(_lib.LIB_PATH, DOMINANT_KERNEL)
+    except Exception:  # no llvm-objdump: counts cannot be matched to the build
+        return None
 
 
 def parse():
@@ -604,7 +605,7 @@ def main():
     osc_slots = n_sin / 64 * OSC_SLOTS_PER_SINE
     vc = load_traffic(args.valu_counts).get(f"config{args.config}", {})
     src_sha = kernel_source_sha()
-    stale = bool(vc) and vc.get("source_sha") != src_sha
+    stale = bool(vc) and (src_sha is None or vc.get("kernel_sha") != src_sha)
     if vc.get("SQ_INSTS_VALU") and not stale:
         slots = vc["SQ_INSTS_VALU"] + (SIN_SLOTS - 1) * n_sin / 64
         slots_src = (f"PMC SQ_INSTS_VALU {vc['SQ_INSTS_VALU']:.4g} wave-instructions per launch "
@@ -612,7 +613,7 @@ def main():
                      "v_sin_f32 wave-instruction")
     else:
         slots = osc_slots
-        slots_src = ("oscillator model only (" + ("the PMC counts were taken on other kernel sources"
+        slots_src = ("oscillator model only (" + ("the PMC counts were taken on another build of the kernel"
                      if stale else "no PMC counts for this configuration") + ")")
     # algorithmic issue slots: per sample H x (6 VALU + v_sin_f32 at 4 slots) for the
     # oscillator + 127 FIR taps (one FMA each) for the noise filter; no controls, RNG or addressing
@@ -627,7 +628,7 @@ def main():
                 "algorithmic_slots_per_launch": round(alg_slots),
                 "algorithmic_slots_note": f"samples/64 x (H x {OSC_SLOTS_PER_SINE} + {fir_taps}): per (sample, "
                                           "harmonic) 6 VALU + v_sin_f32 (4 slots), per sample the 127-tap noise FIR",
-                "valu_counts_source_sha": vc.get("source_sha"), "kernel_source_sha": src_sha,
+                "valu_counts_kernel_sha": vc.get("kernel_sha"), "kernel_sha": src_sha,
                 "traffic": traffic.get("synth_frame_kernel"),
                 "kernel": "synth_frame_kernel (oscillator bank + filtered noise + their controls, fused)",
                 "avg_launch_ms": round(osc_ms, 4), "slots_per_launch": round(slots),

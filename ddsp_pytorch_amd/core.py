@@ -422,6 +422,13 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     return (*res, cd) if parts else (res, cd)
 
 
+def set_persistent_workgroups(per_cu):
+    """Launch shape of the fused synthesis kernel for launches of many frames
+    (ddsp_hip_set_persistent_workgroups): persistent workgroups per CU, 0 = one workgroup per frame,
+    -1 = the default.  Returns the previous setting."""
+    return int(_lib.query("set_persistent_workgroups", int(per_cu)))
+
+
 def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed, bias=-5.0):
     """synth_frames with on-device noise whose Philox offset is the device word counter[0]
     (int64, advanced by one on the stream after the launch): for calls replayed from a captured

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 
 #include "common.h"
 #include "noise_dsp.h"
@@ -157,6 +159,9 @@ __device__ __forceinline__ bool frame_synth(
     // addresses (tools/loop_align.py, pinned by tests/test_loop_align.py); PAD puts
     // one dword of padding after an 8-byte alignment point ahead of it where an instantiation needs
     // it (the alignment makes the placement independent of the code laid out before the kernel)
+#ifdef DDSP_PROBE_CLOCK
+    if (tid == 0) red[20] = (double)wall_clock64();
+#endif
     if constexpr (PAD) asm volatile(".p2align 3\n s_nop 0");
     else asm volatile(".p2align 3");
 #ifdef DDSP_PROBE_NO_OSC
@@ -183,6 +188,9 @@ __device__ __forceinline__ bool frame_synth(
       }
     }
     __syncthreads();  // tail[] complete
+#ifdef DDSP_PROBE_CLOCK
+    if (tid == 0) red[21] = (double)wall_clock64();
+#endif
   } else {
     // SPLIT: every thread takes samples j = tid, tid + NT, ... (the same per-sample sum over k in
     // the same order as above, so the result does not depend on the launch shape); the samples
@@ -256,15 +264,333 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   __shared__ double red[32];
   float acc[4], nz[4];
   int j0;
+#ifdef DDSP_PROBE_CLOCK  // shader clocks and 100 MHz ticks over the workgroup's life (tools/exp_clock.py)
+  const uint64_t pc0 = clock64(), pt0 = wall_clock64();
+#endif
   if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
                                       (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
                                       blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0))
     return;
   const int64_t o = ((int64_t)blockIdx.y * F + blockIdx.x) * bs + j0;
+#ifdef DDSP_PROBE_CLOCK  // harm_out receives the probe: [compute ticks, store ticks, cycles, total ticks]
+  const uint64_t pt1 = wall_clock64();
+#else
   if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
   if (noise_out) *reinterpret_cast<float4*>(noise_out + o) = make_float4(nz[0], nz[1], nz[2], nz[3]);
+#endif
   *reinterpret_cast<float4*>(out + o) =
       make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121
+#ifdef DDSP_PROBE_CLOCK
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t pt2 = wall_clock64();
+  if (threadIdx.x == 0 && harm_out) {
+    *reinterpret_cast<float4*>(harm_out + o) =
+        make_float4((float)(pt0 & 0xFFFFFF), (float)((uint64_t)red[20] - pt0), (float)((uint64_t)red[21] - pt0),
+                    (float)(pt2 - pt0));
+    *reinterpret_cast<float2*>(harm_out + o + 4) = make_float2((float)(pt1 - pt0), (float)(clock64() - pc0));
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent, wave-specialised form of synth_frame_kernel for launches of many frames.
+//
+// Why: one workgroup per frame spends ~2/3 of its life in the frame's prologue (controls, filter
+// design, noise; latency-bound: dependent global loads and workgroup barriers) and ~1/3 in the
+// VALU-bound sine loop.  Across 12800 short-lived workgroups that leaves the VALU idle while the
+// first generation of workgroups all run their prologues at once (~15-20 us at config 2) and while
+// the last generation drains (~35 us of falling occupancy) — measured with DDSP_PROBE_CLOCK
+// (tools/exp_clock.py --in-kernel).  Here a workgroup is NS synthesis threads (the frame's samples,
+// 4 per thread, as above) plus one preparation wave, and it walks a contiguous range of frames:
+// while the synthesis waves run frame i's sine loop and FIR from one LDS frame buffer, the
+// preparation wave builds frame i+1's controls, coefficient table, filter and noise in the other
+// (wave-local synchronisation only), and one workgroup barrier per frame swaps them.  Workgroups
+// get frame ranges that differ by at most one frame, so they finish together, and the phase
+// prefix S_f is carried from frame to frame (exact: every partial sum is representable).
+// Arithmetic per sample is the same as synth_frame_kernel's (the noise-filter normalisation sums in
+// another order: the control values' double sum may round differently in the last bit).
+
+// LDS-visibility point for one wave: its LDS writes done before any lane's later reads
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double wave_sum_double(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Frame buffer layout (floats): coef float2[H4] | ct[n4] | A[NB->4] | ir[half+1->4] | h[bs] | tail[half->4] |
+// xbuf[pad | bs] | scalars (double S, double dinc) at the end (buf_floats, a multiple of 4, includes them)
+struct FrameBuf {
+  float* base;
+  int o_ct, o_A, o_ir, o_h, o_tail, o_x, o_sc;  // float offsets (workgroup-uniform)
+  __device__ FrameBuf(float* b, int H4, int n4, int NB, int half, int bs, int pad, int buf_floats) : base(b) {
+    o_ct = 2 * H4;
+    o_A = o_ct + n4;
+    o_ir = o_A + ((NB + 3) & ~3);
+    o_h = o_ir + ((half + 4) & ~3);
+    o_tail = o_h + bs;
+    o_x = o_tail + ((half + 3) & ~3) + pad;
+    o_sc = buf_floats - 4;
+  }
+  __device__ float2* coef() const { return reinterpret_cast<float2*>(base); }
+  __device__ float* ct() const { return base + o_ct; }
+  __device__ float* A() const { return base + o_A; }
+  __device__ float* ir() const { return base + o_ir; }
+  __device__ float* h() const { return base + o_h; }
+  __device__ float* tail() const { return base + o_tail; }
+  __device__ float* x() const { return base + o_x; }
+  __device__ double* sc() const { return reinterpret_cast<double*>(base + o_sc); }
+};
+
+// The preparation wave (lane in [0, 64)): everything frame_synth does before its sine loop, for one
+// frame, into buffer fb.  carry: this frame follows the one prepared before it in the same row, whose
+// prefix was carry_S.  Returns this frame's prefix S.
+template <bool RNG, bool CTRL>
+__device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const float* __restrict__ param,
+                                           const float* __restrict__ mags, float bias,
+                                           const float* __restrict__ noise, uint32_t k0, uint32_t k1,
+                                           uint32_t off0, uint32_t off1, float* __restrict__ ctrl_out, int B,
+                                           int F, int H, int NB, int bs, float sr, int lo_end, int tail_start,
+                                           int pad, int frame, FrameBuf fb, int lane, bool carry,
+                                           double carry_S) {
+  const int n = 2 * (NB - 1), half = n >> 1;
+  const int H4 = (H + 3) & ~3;
+  const int b = frame / F, f = frame - b * F;
+  const float* f0b = f0 + (int64_t)b * F;
+  const float* prow = param + (int64_t)frame * (H + 1);
+  const float half_sr = sr * 0.5f;
+  const float pitch0 = f0b[f];
+#ifdef DDSP_PROBE_CLOCK
+  uint64_t pts[6];
+  pts[0] = wall_clock64();
+#endif
+  // exact fp64 prefix over the row's earlier frames, carried from the previous frame when it is the
+  // one before this in the same row
+  double S;
+  if (f == 0) {
+    S = 0.0;
+  } else if (carry) {
+    S = carry_S + (double)bs * (double)phase_inc(f0b[f - 1], sr);
+  } else {
+    double part = 0.0;
+    for (int g = lane; g < f; g += 64) part += (double)bs * (double)phase_inc(f0b[g], sr);
+    S = wave_sum_double(part);
+  }
+  // controls (modules.py:44-61, 111-114), cosine table, noise (modules.py:119-123)
+  double part_d = 0.0;
+  for (int k = lane; k < H; k += 64) {
+    const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+    fb.coef()[k].y = v;
+    part_d += (double)v;
+  }
+  for (int k = lane; k < NB; k += 64) fb.A()[k] = scale_fn(mags[(int64_t)frame * NB + k] + bias);
+  fill_cos_table(fb.ct(), n, lane, 64);
+  for (int i = lane; i < pad; i += 64) fb.x()[i - pad] = 0.0f;
+  const int quads = bs >> 2;
+  for (int t = lane; t < quads; t += 64) {
+    float4 v;
+    if (RNG) {
+      const uint64_t q = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
+      const Philox4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
+      v = make_float4(uniform_pm1(r.v[0]), uniform_pm1(r.v[1]), uniform_pm1(r.v[2]), uniform_pm1(r.v[3]));
+    } else {
+      v = *reinterpret_cast<const float4*>(noise + (int64_t)frame * bs + 4 * t);
+    }
+    *reinterpret_cast<float4*>(fb.x() + 4 * t) = v;
+  }
+  const float norm = (float)wave_sum_double(part_d);  // dist.sum(-1)
+  const float a = scale_fn(prow[0]);
+  for (int k = lane; k < H4; k += 64) {  // each lane rereads only the values it wrote
+    const float v = k < H ? (fb.coef()[k].y / norm) * a : 0.0f;  // (dist / sum) * amp
+    fb.coef()[k] = make_float2((float)(k + 1), v);
+  }
+  wave_lds_sync();  // A, ct, x
+#ifdef DDSP_PROBE_CLOCK
+  pts[1] = wall_clock64();
+#endif
+  // filter design (core.py:144-166): the irfft's even half, then the rolled/windowed taps
+  if (n == 128) {
+    // 65 bands: lane m builds tap m from the global irfft matrix (coalesced rows of 64); the rows are read
+    // through an opaque zero offset, so the compiler cannot hoist the 63 loop-invariant loads out of the
+    // frame loop into registers the whole kernel would then hold
+    int zero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+    const float* cosm = kIrCos128 + lane + zero;
+    const float* A = fb.A();
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 8
+    for (int k = 1; k < 63; k += 2) {
+      s0 = fmaf(A[k], cosm[k * 64], s0);
+      s1 = fmaf(A[k + 1], cosm[(k + 1) * 64], s1);
+    }
+    s0 = fmaf(A[63], cosm[63 * 64], s0);
+    fb.ir()[lane] = (A[0] + ((lane & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
+    float alt = (lane >= 1) ? ((lane & 1) ? -A[lane] : A[lane]) : 0.0f;  // tap n/2: cos(pi k) = (-1)^k
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
+    if (lane == 0) fb.ir()[64] = (A[0] + A[64] + 2.0f * alt) * (1.0f / 128.0f);
+  } else {
+    for (int m = lane; m <= half; m += 64) fb.ir()[m] = irfft_tap(fb.A(), fb.ct(), n, m);
+  }
+  wave_lds_sync();  // ir
+#ifdef DDSP_PROBE_CLOCK
+  pts[2] = wall_clock64();
+#endif
+  const int nlo = lo_end, ntaps = lo_end + (bs - tail_start);
+  for (int i = lane; i < ntaps; i += 64) {
+    const int j = i < nlo ? i : tail_start + (i - nlo);
+    fb.h()[j] = ir_at_half(fb.ir(), fb.ct(), n, bs, j);
+  }
+  wave_lds_sync();  // h
+#ifdef DDSP_PROBE_CLOCK
+  pts[3] = wall_clock64();
+#endif
+  // noise tail: taps past bs - n/2 reach only the last n/2 outputs
+  for (int l = lane; l < bs - tail_start; l += 64) {
+    const int j = tail_start + l;
+    float c = 0.0f;
+    for (int d = 0; d <= l; ++d) c = fmaf(fb.h()[j - d], fb.x()[d], c);
+    fb.tail()[l] = c;
+  }
+  if (lane == 0) {
+    fb.sc()[0] = S;
+    fb.sc()[1] = (double)phase_inc(pitch0, sr);
+  }
+#ifdef DDSP_PROBE_CLOCK  // prep phase durations of this frame -> ctrl_out[8 * frame ..] (probe builds only)
+  pts[4] = wall_clock64();
+  if (lane == 0 && ctrl_out) {
+    for (int i = 0; i < 4; ++i) ctrl_out[8 * (int64_t)frame + i] = (float)(pts[i + 1] - pts[i]);
+  }
+  return S;
+#endif
+  if constexpr (CTRL) {  // the controls the reference returns (decoder.py:127-135)
+    const int64_t BF = (int64_t)B * F;
+    if (lane == 0) ctrl_out[frame] = a;
+    for (int k = lane; k < H; k += 64) ctrl_out[BF + (int64_t)frame * H + k] = fb.coef()[k].y;
+    for (int k = lane; k < NB; k += 64) ctrl_out[BF * (1 + H) + (int64_t)frame * NB + k] = fb.A()[k];
+  }
+  return S;
+}
+
+template <bool RNG, bool CTRL, bool PAD>
+__global__ void __launch_bounds__(320, 6) synth_persist_kernel(
+    const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
+    float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
+    const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
+    float* __restrict__ noise_out, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs, float sr,
+    int lo_end, int tail_start, int pad, int buf_floats) {
+  extern __shared__ float4 smem4[];
+  const int NS = (int)blockDim.x - 64;  // synthesis threads; the last wave prepares
+  const int tid = threadIdx.x;
+  const bool prep = tid >= NS;
+  const int lane = tid & 63;
+  const int NF = B * F;
+  const int first = (int)(((int64_t)blockIdx.x * NF) / gridDim.x);
+  const int last = (int)(((int64_t)(blockIdx.x + 1) * NF) / gridDim.x);
+  const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
+  const int H4 = (H + 3) & ~3;
+  float* base = reinterpret_cast<float*>(smem4);
+  FrameBuf fb0(base, H4, n4, NB, half, bs, pad, buf_floats), fb1 = fb0;
+  fb1.base = base + buf_floats;
+  double carry_S = 0.0;
+  if (RNG && counter) {  // graph-replayed streams: the Philox offset advances in device memory
+    const uint64_t o = (((uint64_t)off1 << 32) | off0) + *counter;
+    off0 = (uint32_t)o;
+    off1 = (uint32_t)(o >> 32);
+  }
+#ifdef DDSP_PROBE_HWID  // each wave's HW_ID (SIMD, CU, SE) -> harm_out[4 * workgroup + wave]
+  if (lane == 0 && harm_out)
+    harm_out[4 * (int64_t)blockIdx.x + (tid >> 6)] = __int_as_float((int)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  if (harm_out) return;
+#endif
+  // iteration fr: the preparation wave builds frame fr + 1, the synthesis waves run frame fr; one barrier
+  // per iteration.  The two roles run separate loops (same trip count, so the same barriers) so that each
+  // loop's hoisted invariants stay in its own branch and do not hold registers through the sine loop.
+  if (prep) {
+    for (int fr = first - 1; fr < last; ++fr) {
+#ifdef DDSP_PROBE_NO_PREP  // timing probe: only the first frame is prepared
+      if (fr + 1 < last && fr < first) {
+#else
+      if (fr + 1 < last) {
+#endif
+        FrameBuf nb = fb0;
+        nb.base = ((fr + 1 - first) & 1) ? fb1.base : fb0.base;  // frame fr + 1's
+        carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
+                                        bs, sr, lo_end, tail_start, pad, fr + 1, nb, lane, fr >= first, carry_S);
+      }
+      __syncthreads();  // frame fr's buffer free, frame fr + 1's prepared
+    }
+    return;
+  }
+  __syncthreads();  // the first frame prepared
+  const int j0 = 4 * tid;
+  for (int fr = first; fr < last; ++fr) {
+    FrameBuf cur = fb0;
+    cur.base = ((fr - first) & 1) ? fb1.base : fb0.base;
+#ifdef DDSP_PROBE_CLOCK
+    const uint64_t st0 = wall_clock64();
+#endif
+    if (j0 < bs) {
+      const double S = cur.sc()[0], dinc = cur.sc()[1];
+      float w[4], acc[4];
+      bool fast = true;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        w[s] = (float)(S + (double)(j0 + s + 1) * dinc);  // omega = fl32(exact prefix)
+        acc[s] = 0.0f;
+        fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
+      }
+      const float2* coef = cur.coef();
+      // loop placement as in frame_synth (tests/test_loop_align.py pins it)
+      if constexpr (PAD) asm volatile(".p2align 3\n s_nop 0");
+      else asm volatile(".p2align 3");
+#ifdef DDSP_PROBE_NO_OSC  // timing probe: no sine loop
+      if (false)
+#endif
+      if (fast) {
+#pragma unroll 4
+        for (int k = 0; k < H4; ++k) {
+          const float2 c = coef[k];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
+        }
+      } else {
+        for (int k = 0; k < H; ++k) {
+          const float2 c = coef[k];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const float xx = w[s] * c.x;
+            acc[s] = fmaf(fabsf(xx) < kFastArgLimit ? sin_reduced(xx) : sin_slow(xx), c.y, acc[s]);
+          }
+        }
+      }
+      const float4 y = fir4(cur.h(), cur.x(), j0, lo_end, bs, bs);  // taps [0, lo_end); wrapped ones in tail[]
+      float nz[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (j0 + s >= tail_start) nz[s] += cur.tail()[j0 + s - tail_start];
+      const int64_t o = (int64_t)fr * bs + j0;
+      if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (noise_out) *reinterpret_cast<float4*>(noise_out + o) = make_float4(nz[0], nz[1], nz[2], nz[3]);
+      *reinterpret_cast<float4*>(out + o) =
+          make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121
+    }
+#ifdef DDSP_PROBE_CLOCK  // synthesis time and barrier wait of this frame -> ctrl_out[8 * frame + 4, 5]
+    const uint64_t st1 = wall_clock64();
+    __syncthreads();
+    if (tid == 0 && ctrl_out) {
+      ctrl_out[8 * (int64_t)fr + 4] = (float)(st1 - st0);
+      ctrl_out[8 * (int64_t)fr + 5] = (float)(wall_clock64() - st1);
+    }
+#else
+    __syncthreads();  // frame fr's buffer free, frame fr + 1's prepared
+#endif
+  }
 }
 
 __global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
@@ -273,6 +599,45 @@ __global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
 }  // namespace ddsp
 
 using namespace ddsp;
+
+// sine-loop placement padding of the persistent instantiations (tools/loop_align.py)
+template <bool RNG, bool CTRL>
+constexpr bool kPersistPad = false;
+
+// compute units of the current device (cached per device)
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// persistent workgroups per CU: ddsp_hip_set_persistent_workgroups, else DDSP_HIP_PERSIST_WPC, else 8
+// (0 turns the persistent kernel off)
+static std::atomic<int> g_persist_wpc{-1};
+static int persist_default() {
+  const char* e = getenv("DDSP_HIP_PERSIST_WPC");
+  return e ? std::max(0, atoi(e)) : 0;  // off by default until it beats the per-frame kernel
+}
+static int persist_wgs_per_cu() {
+  const int v = g_persist_wpc.load(std::memory_order_relaxed);
+  return v >= 0 ? v : persist_default();
+}
+
+// DDSP_HIP_PERSIST_LDSPAD=1: LDS per workgroup padded so that a CU holds at most wpc of them
+static size_t persist_lds_floor(int wpc) {
+  static int pad = -1;
+  if (pad < 0) {
+    const char* e = getenv("DDSP_HIP_PERSIST_LDSPAD");
+    pad = e ? atoi(e) : 0;
+  }
+  return pad && wpc > 0 ? (size_t)(160 * 1024 / (wpc + 1) + 1024) : 0;
+}
 
 extern "C" {
 
@@ -313,6 +678,32 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   const size_t shm = sizeof(float) * (floats + (G > 1 ? (size_t)bs : 0));
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
+  // many frames: the persistent, wave-specialised kernel (frame ranges per workgroup)
+  const int64_t NF = batch * frames;
+  const int cus = device_cus();
+  const int wpc = persist_wgs_per_cu();
+  const int buf_floats = (int)((floats + 4 + 3) & ~(size_t)3);
+  const size_t pshm = sizeof(float) * 2 * (size_t)buf_floats;
+  if (G == 1 && wpc > 0 && cus > 0 && NF <= INT32_MAX && NF >= 2LL * cus * wpc && pshm <= 64 * 1024) {
+    const int pgrid = cus * wpc;
+    const size_t lds = std::max(pshm, persist_lds_floor(wpc));
+    const dim3 pblock((unsigned)(nt + 64));
+#define DDSP_SYNTH_PERSIST_LAUNCH(RNG_, CTRL_)                                                              \
+    hipLaunchKernelGGL((synth_persist_kernel<RNG_, CTRL_, kPersistPad<RNG_, CTRL_>>), dim3(pgrid), pblock, lds, \
+                       S(stream), f0, param, raw_magnitudes, bias, RNG_ ? nullptr : noise, k0, k1, o0, o1,      \
+                       RNG_ ? counter : nullptr, out, harmonic_out, noise_out, controls_out, (int)batch,          \
+                       (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats)
+    if (noise) {
+      if (controls_out) DDSP_SYNTH_PERSIST_LAUNCH(false, true);
+      else DDSP_SYNTH_PERSIST_LAUNCH(false, false);
+    } else {
+      if (controls_out) DDSP_SYNTH_PERSIST_LAUNCH(true, true);
+      else DDSP_SYNTH_PERSIST_LAUNCH(true, false);
+    }
+#undef DDSP_SYNTH_PERSIST_LAUNCH
+    if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
+    return launch_status();
+  }
   const dim3 grid((unsigned)frames, (unsigned)batch), block((unsigned)(nt * G));
 #define DDSP_SYNTH_FRAME_LAUNCH(RNG_, SPLIT_)                                                              \
   do {                                                                                                  \
@@ -335,6 +726,10 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
 #undef DDSP_SYNTH_FRAME_LAUNCH_
   if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
   return launch_status();
+}
+
+int ddsp_hip_set_persistent_workgroups(int per_cu) {
+  return g_persist_wpc.exchange(per_cu < 0 ? -1 : per_cu);
 }
 
 int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,

@@ -140,6 +140,13 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                           int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                           void* stream);
 
+/* Launch shape of ddsp_hip_synth_frames* for many frames (>= 2 x CUs x per_cu): per_cu persistent
+ * workgroups per compute unit, each a preparation wave (controls, filter design, noise of the next
+ * frame) beside the synthesis waves of the current one; 0 selects one workgroup per frame for every
+ * launch; -1 restores the default (DDSP_HIP_PERSIST_WPC, else 0).  Process-wide (an atomic; safe from
+ * any thread, applies to later launches); returns the previous setting. */
+int ddsp_hip_set_persistent_workgroups(int per_cu);
+
 /* ddsp_hip_synth_frames that also writes the controls DDSPDecoder.forward returns
  * (decoder.py:127-135: output['harmonic_ctrls'], output['noise_ctrls']) into controls_out (nullable),
  * laid out as [amplitudes B*F | harmonic_distribution B*F*H | magnitudes B*F*NB]: amplitudes =

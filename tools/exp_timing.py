@@ -61,6 +61,9 @@ def main():
     print(f"B synth, events around each launch      : {per_launch(synth):7.1f} us", flush=True)
     settle(lambda: (synth(), reverb()))
     print(f"C synth then reverb, events around synth: {per_launch(synth, reverb):7.1f} us", flush=True)
+    if "--short" in sys.argv:
+        print(f"E synth+reverb step group               : {group(lambda: (synth(), reverb())):7.1f} us", flush=True)
+        return
     print(f"D reverb group                          : {group(reverb):7.1f} us", flush=True)
     print(f"E synth+reverb step group               : {group(lambda: (synth(), reverb())):7.1f} us", flush=True)
     def synced():

@@ -14,8 +14,8 @@ import sys
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
-    """the kernel's sine loop: start address, size, 8-byte instructions at odd dword addresses"""
+def kernel_instructions(so, kern):
+    """[(address, bytes, text)] of one kernel's instructions in the library's gfx950 code object"""
     tmp = tempfile.mkdtemp()
     local = os.path.join(tmp, os.path.basename(so))
     shutil.copy(so, local)
@@ -37,6 +37,26 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
     for l in out:
         m=re.search(r"//\s*([0-9A-F]+):\s*((?:[0-9A-F]{8}\s*)+)",l)
         if m: ins.append((int(m.group(1),16), len(m.group(2).split())*4, l.split("//")[0].strip()))
+    return ins
+
+
+def kernel_sha(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
+    """sha256 (16 hex) of one kernel's instruction stream (text and sizes, addresses relative to its
+    entry): the key under which PMC counts of that kernel stay valid (bench.py, pmc_valu.py)"""
+    import hashlib
+    ins = kernel_instructions(so, kern)
+    if not ins:
+        return None
+    base = ins[0][0]
+    h = hashlib.sha256()
+    for addr, size, txt in ins:
+        h.update(f"{addr - base} {size} {txt}\n".encode())
+    return h.hexdigest()[:16]
+
+
+def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
+    """the kernel's sine loop: start address, size, 8-byte instructions at odd dword addresses"""
+    ins = kernel_instructions(so, kern)
     # the hot loop: the innermost backward-branch loop holding >= 8 v_sin_f32
     best = None
     for i, (addr, size, txt) in enumerate(ins):

@@ -28,10 +28,10 @@ def main():
     except (OSError, ValueError):
         out = {}
     sys.path.insert(0, ROOT)
-    from bench import kernel_source_sha
-    out[f"config{cfg}"] = {"kernel": "synth_frame_kernel<true,false,false>",
+    from bench import DOMINANT_KERNEL, kernel_source_sha
+    out[f"config{cfg}"] = {"kernel": DOMINANT_KERNEL,
                            "source": os.path.relpath(d, ROOT).replace("gpurun_out/", "profiles/") + ".txt",
-                           "source_sha": kernel_source_sha(),
+                           "kernel_sha": kernel_source_sha(),
                            **{k: m[k] for k in sorted(m) if k.startswith("SQ_")}}
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out[f"config{cfg}"], indent=1))
