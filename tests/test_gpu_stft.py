@@ -179,6 +179,13 @@ def test_spectral_loss_grad_well_conditioned_bins(dd):
     masked_loss(dd.core.multiscale_fft(sig32.cuda(), scales, ov), dd.core.multiscale_fft(rg, scales, ov),
                 dd.core.safe_log).backward()
     assert relerr(rg.grad, ref32) < 1e-5, relerr(rg.grad, ref32)
+    # ... and against the reference itself: golden g7b is this masked loss's gradient computed by the
+    # reference's multiscale_fft / safe_log (tests/golden/make_goldens.py masked_loss_golden), its masks
+    # stored with it
+    g7b = load_golden("g7b_stft_loss_masked")
+    for s_, m in zip(scales, masks):
+        assert torch.equal(torch.as_tensor(g7b[f"mask_{s_}"]).float(), m), s_
+    assert relerr(rg.grad, g7b["grad_rec"]) < 1e-5, relerr(rg.grad, g7b["grad_rec"])
     # unmasked: the fused kernel's gradient is as close to the fp64 gradient as the reference's own
     rc64 = rec32.double().clone().requires_grad_(True)
     tr.multiscale_spec_loss(tr.multiscale_fft(sig32.double(), scales, ov), tr.multiscale_fft(rc64, scales, ov)).backward()

@@ -68,3 +68,21 @@ def test_stft_loss_oracle():
     assert torch.equal(loss.detach(), T(g["loss"]))
     loss.backward()
     assert relerr(rec.grad, g["grad_rec"]) < 1e-6
+
+
+def test_masked_stft_loss_oracle():
+    """The oracle reproduces the reference's masked-loss gradient (g7b: train.py's loss on the
+    well-conditioned bins, tests/golden/make_goldens.py masked_loss_golden) bit for bit."""
+    g = load_golden("g7_stft_loss")
+    gb = load_golden("g7b_stft_loss_masked")
+    scales, overlap = [int(s) for s in g["scales"]], float(g["overlap"])
+    rec = T(g["rec"]).clone().requires_grad_(True)
+    ori = tr.multiscale_fft(T(g["sig"]), scales, overlap)
+    rs = tr.multiscale_fft(rec, scales, overlap)
+    loss = 0
+    for s, mx, my in zip(scales, ori, rs):
+        m = T(gb[f"mask_{s}"]).float()
+        loss = loss + (m * (mx - my).abs()).mean() + (m * (tr.safe_log(mx) - tr.safe_log(my)).abs()).mean()
+    assert torch.equal(loss.detach(), T(gb["loss"]))
+    loss.backward()
+    assert torch.equal(rec.grad, T(gb["grad_rec"]))
