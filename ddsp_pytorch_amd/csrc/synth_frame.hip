@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 
 #include "common.h"
@@ -324,7 +326,8 @@ __device__ __forceinline__ double wave_sum_double(double v) {
 }
 
 // Frame buffer layout (floats): coef float2[H4] | ct[n4] | A[NB->4] | ir[half+1->4] | h[bs] | tail[half->4] |
-// xbuf[pad | bs] | scalars (double S, double dinc) at the end (buf_floats, a multiple of 4, includes them)
+// xbuf[pad | bs] | scalars (double S, double dinc, int frame) in the last 8 floats (buf_floats, a multiple
+// of 4, includes them)
 struct FrameBuf {
   float* base;
   int o_ct, o_A, o_ir, o_h, o_tail, o_x, o_sc;  // float offsets (workgroup-uniform)
@@ -335,7 +338,7 @@ struct FrameBuf {
     o_h = o_ir + ((half + 4) & ~3);
     o_tail = o_h + bs;
     o_x = o_tail + ((half + 3) & ~3) + pad;
-    o_sc = buf_floats - 4;
+    o_sc = buf_floats - 8;
   }
   __device__ float2* coef() const { return reinterpret_cast<float2*>(base); }
   __device__ float* ct() const { return base + o_ct; }
@@ -345,6 +348,7 @@ struct FrameBuf {
   __device__ float* tail() const { return base + o_tail; }
   __device__ float* x() const { return base + o_x; }
   __device__ double* sc() const { return reinterpret_cast<double*>(base + o_sc); }
+  __device__ int* frame() const { return reinterpret_cast<int*>(base + o_sc + 4); }  // -1: no more frames
 };
 
 // The preparation wave (lane in [0, 64)): everything frame_synth does before its sine loop, for one
@@ -364,34 +368,27 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
   const float* f0b = f0 + (int64_t)b * F;
   const float* prow = param + (int64_t)frame * (H + 1);
   const float half_sr = sr * 0.5f;
-  const float pitch0 = f0b[f];
 #ifdef DDSP_PROBE_CLOCK
   uint64_t pts[6];
   pts[0] = wall_clock64();
 #endif
-  // exact fp64 prefix over the row's earlier frames, carried from the previous frame when it is the
-  // one before this in the same row
-  double S;
-  if (f == 0) {
-    S = 0.0;
-  } else if (carry) {
-    S = carry_S + (double)bs * (double)phase_inc(f0b[f - 1], sr);
-  } else {
-    double part = 0.0;
-    for (int g = lane; g < f; g += 64) part += (double)bs * (double)phase_inc(f0b[g], sr);
-    S = wave_sum_double(part);
+  // every global load of the frame's first phase is issued before any of its uses (the compiler keeps
+  // program order here: one memory latency for the phase instead of one per dependent load)
+  const float pitch0 = f0b[f];
+  const float praw0 = prow[0];
+  const bool loop_prefix = f > 0 && !carry;
+  const float fprev = (f > 0 && carry) ? f0b[f - 1] : 0.0f;
+  float fv[4], pv[2], mv[2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) fv[r] = (loop_prefix && lane + 64 * r < f) ? f0b[lane + 64 * r] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int k = lane + 64 * r;
+    pv[r] = k < H ? prow[1 + k] : 0.0f;
+    mv[r] = k < NB ? mags[(int64_t)frame * NB + k] : 0.0f;
   }
-  // controls (modules.py:44-61, 111-114), cosine table, noise (modules.py:119-123)
-  double part_d = 0.0;
-  for (int k = lane; k < H; k += 64) {
-    const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
-    fb.coef()[k].y = v;
-    part_d += (double)v;
-  }
-  for (int k = lane; k < NB; k += 64) fb.A()[k] = scale_fn(mags[(int64_t)frame * NB + k] + bias);
-  fill_cos_table(fb.ct(), n, lane, 64);
-  for (int i = lane; i < pad; i += 64) fb.x()[i - pad] = 0.0f;
   const int quads = bs >> 2;
+  // noise (modules.py:119-123): Philox while the loads are in flight, or the injected samples
   for (int t = lane; t < quads; t += 64) {
     float4 v;
     if (RNG) {
@@ -403,8 +400,43 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
     }
     *reinterpret_cast<float4*>(fb.x() + 4 * t) = v;
   }
+  for (int i = lane; i < pad; i += 64) fb.x()[i - pad] = 0.0f;
+  fill_cos_table(fb.ct(), n, lane, 64);
+  // exact fp64 prefix over the row's earlier frames, carried from the previous frame when it is the
+  // one before this in the same row
+  double S;
+  if (f == 0) {
+    S = 0.0;
+  } else if (carry) {
+    S = carry_S + (double)bs * (double)phase_inc(fprev, sr);
+  } else {
+    double part = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (lane + 64 * r < f) part += (double)bs * (double)phase_inc(fv[r], sr);
+    for (int g = lane + 256; g < f; g += 64) part += (double)bs * (double)phase_inc(f0b[g], sr);  // f > 256
+    S = wave_sum_double(part);
+  }
+  // controls (modules.py:44-61, 111-114)
+  double part_d = 0.0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int k = lane + 64 * r;
+    if (k < H) {
+      const float v = controls_value(pv[r], pitch0, k, half_sr);
+      fb.coef()[k].y = v;
+      part_d += (double)v;
+    }
+    if (k < NB) fb.A()[k] = scale_fn(mv[r] + bias);
+  }
+  for (int k = lane + 128; k < H; k += 64) {  // H > 128
+    const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+    fb.coef()[k].y = v;
+    part_d += (double)v;
+  }
+  for (int k = lane + 128; k < NB; k += 64) fb.A()[k] = scale_fn(mags[(int64_t)frame * NB + k] + bias);
   const float norm = (float)wave_sum_double(part_d);  // dist.sum(-1)
-  const float a = scale_fn(prow[0]);
+  const float a = scale_fn(praw0);
   for (int k = lane; k < H4; k += 64) {  // each lane rereads only the values it wrote
     const float v = k < H ? (fb.coef()[k].y / norm) * a : 0.0f;  // (dist / sum) * amp
     fb.coef()[k] = make_float2((float)(k + 1), v);
@@ -423,12 +455,24 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
     const float* cosm = kIrCos128 + lane + zero;
     const float* A = fb.A();
     float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll 8
-    for (int k = 1; k < 63; k += 2) {
-      s0 = fmaf(A[k], cosm[k * 64], s0);
-      s1 = fmaf(A[k + 1], cosm[(k + 1) * 64], s1);
+    // rows k = 1..64 in 4 batches of 16: each batch's loads issued together, then its FMAs in the order
+    // of the per-frame kernel (s0 odd k, s1 even k, then k = 63 into s0)
+#pragma unroll
+    for (int kb = 1; kb < 65; kb += 16) {
+      float cv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cv[r] = kb + r < 64 ? cosm[(kb + r) * 64] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int k = kb + r;
+        if (k < 63) {
+          s0 = fmaf(A[k], cv[r], s0);
+          s1 = fmaf(A[k + 1], cv[r + 1], s1);
+        } else if (k == 63) {
+          s0 = fmaf(A[63], cv[r], s0);
+        }
+      }
     }
-    s0 = fmaf(A[63], cosm[63 * 64], s0);
     fb.ir()[lane] = (A[0] + ((lane & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
     float alt = (lane >= 1) ? ((lane & 1) ? -A[lane] : A[lane]) : 0.0f;  // tap n/2: cos(pi k) = (-1)^k
 #pragma unroll
@@ -453,8 +497,21 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
   // noise tail: taps past bs - n/2 reach only the last n/2 outputs
   for (int l = lane; l < bs - tail_start; l += 64) {
     const int j = tail_start + l;
+    const float* hh = fb.h();
+    const float* xx = fb.x();
     float c = 0.0f;
-    for (int d = 0; d <= l; ++d) c = fmaf(fb.h()[j - d], fb.x()[d], c);
+    // 8 taps' operands loaded per step, then the FMAs in the per-frame kernel's order (d = 0, 1, ...)
+    for (int d0 = 0; d0 <= l; d0 += 8) {
+      float hv[8], xv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        hv[r] = hh[j - d0 - r];  // (in-buffer for d past l: never used)
+        xv[r] = xx[d0 + r];
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (d0 + r <= l) c = fmaf(hv[r], xv[r], c);
+    }
     fb.tail()[l] = c;
   }
   if (lane == 0) {
@@ -478,26 +535,23 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
 }
 
 template <bool RNG, bool CTRL, bool PAD>
-__global__ void __launch_bounds__(320, 6) synth_persist_kernel(
+__global__ void __launch_bounds__(320, 5) synth_persist_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
     float* __restrict__ noise_out, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs, float sr,
-    int lo_end, int tail_start, int pad, int buf_floats) {
+    int lo_end, int tail_start, int pad, int buf_floats, uint32_t* __restrict__ tickets) {
   extern __shared__ float4 smem4[];
   const int NS = (int)blockDim.x - 64;  // synthesis threads; the last wave prepares
   const int tid = threadIdx.x;
   const bool prep = tid >= NS;
   const int lane = tid & 63;
   const int NF = B * F;
-  const int first = (int)(((int64_t)blockIdx.x * NF) / gridDim.x);
-  const int last = (int)(((int64_t)(blockIdx.x + 1) * NF) / gridDim.x);
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
   float* base = reinterpret_cast<float*>(smem4);
   FrameBuf fb0(base, H4, n4, NB, half, bs, pad, buf_floats), fb1 = fb0;
   fb1.base = base + buf_floats;
-  double carry_S = 0.0;
   if (RNG && counter) {  // graph-replayed streams: the Philox offset advances in device memory
     const uint64_t o = (((uint64_t)off1 << 32) | off0) + *counter;
     off0 = (uint32_t)o;
@@ -508,30 +562,69 @@ __global__ void __launch_bounds__(320, 6) synth_persist_kernel(
     harm_out[4 * (int64_t)blockIdx.x + (tid >> 6)] = __int_as_float((int)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   if (harm_out) return;
 #endif
-  // iteration fr: the preparation wave builds frame fr + 1, the synthesis waves run frame fr; one barrier
-  // per iteration.  The two roles run separate loops (same trip count, so the same barriers) so that each
-  // loop's hoisted invariants stay in its own branch and do not hold registers through the sine loop.
-  if (prep) {
-    for (int fr = first - 1; fr < last; ++fr) {
-#ifdef DDSP_PROBE_NO_PREP  // timing probe: only the first frame is prepared
-      if (fr + 1 < last && fr < first) {
-#else
-      if (fr + 1 < last) {
+  // Frames are taken one at a time from the launch's ticket counter (tickets[0]) by the preparation
+  // wave, so workgroups whose SIMDs carry more synthesis waves take fewer frames (dynamic balance, as a
+  // one-workgroup-per-frame launch has).  The workgroup that takes the last failing ticket (tickets[1]
+  // counts them) zeroes both counters for the stream's next launch.  Iteration i: the preparation wave
+  // builds the next frame in buffer (i+1)&1 while the synthesis waves run buffer i&1's; one barrier per
+  // iteration.  The two roles run separate loops (the same number of barriers) so that each loop's
+  // hoisted invariants stay in its own branch and hold no registers through the sine loop.
+#ifdef DDSP_PROBE_CLOCK
+  const uint64_t wg_t0 = wall_clock64();
+  int probe_first = -1;
 #endif
-        FrameBuf nb = fb0;
-        nb.base = ((fr + 1 - first) & 1) ? fb1.base : fb0.base;  // frame fr + 1's
-        carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
-                                        bs, sr, lo_end, tail_start, pad, fr + 1, nb, lane, fr >= first, carry_S);
+  if (prep) {
+    // the preparation wave's instructions issue ahead of the synthesis waves' (VALU arbitration is by
+    // priority, then age): its chain of short dependent steps then waits on memory and LDS only, not on
+    // the sine loops that saturate the SIMD
+    __builtin_amdgcn_s_setprio(3);
+    auto take = [&]() -> int {
+      int t = 0;
+      if (lane == 0) t = (int)atomicAdd(tickets, 1u);
+      t = __shfl(t, 0, 64);
+      if (t >= NF) {
+        if (lane == 0 && atomicAdd(tickets + 1, 1u) == gridDim.x - 1) {  // every workgroup is done taking
+          tickets[0] = 0;
+          tickets[1] = 0;
+        }
+        return -1;
       }
-      __syncthreads();  // frame fr's buffer free, frame fr + 1's prepared
+      return t;
+    };
+    int prev = -2;
+    double carry_S = 0.0;
+    int fr = take();
+    for (int i = 0;; ++i) {
+      FrameBuf nb = fb0;
+      nb.base = (i & 1) ? fb1.base : fb0.base;
+      if (fr >= 0) {
+#ifdef DDSP_PROBE_CLOCK
+        if (probe_first < 0) probe_first = fr;
+#endif
+        carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
+                                        bs, sr, lo_end, tail_start, pad, fr, nb, lane, fr == prev + 1, carry_S);
+      }
+      if (lane == 0) *nb.frame() = fr;
+      __syncthreads();  // buffer i&1 prepared (or marked empty); the synthesis waves released the other one
+      if (fr < 0) break;
+      prev = fr;
+      fr = take();
     }
+#ifdef DDSP_PROBE_CLOCK  // workgroup start (low 24 bits of the 100 MHz clock) and life -> ctrl_out[8 * first + 6, 7]
+    if (lane == 0 && ctrl_out && probe_first >= 0) {
+      ctrl_out[8 * (int64_t)probe_first + 6] = (float)(wg_t0 & 0xFFFFFF);
+      ctrl_out[8 * (int64_t)probe_first + 7] = (float)(wall_clock64() - wg_t0);
+    }
+#endif
     return;
   }
   __syncthreads();  // the first frame prepared
   const int j0 = 4 * tid;
-  for (int fr = first; fr < last; ++fr) {
+  for (int i = 0;; ++i) {
     FrameBuf cur = fb0;
-    cur.base = ((fr - first) & 1) ? fb1.base : fb0.base;
+    cur.base = (i & 1) ? fb1.base : fb0.base;
+    const int fr = *cur.frame();
+    if (fr < 0) break;
 #ifdef DDSP_PROBE_CLOCK
     const uint64_t st0 = wall_clock64();
 #endif
@@ -629,6 +722,27 @@ static int persist_wgs_per_cu() {
   return v >= 0 ? v : persist_default();
 }
 
+// The persistent kernel's ticket counters (frames taken, workgroups done), one pair per (device, stream):
+// zeroed once here, then by the last workgroup of every launch, so launches on one stream (ordered) reuse
+// them; a device allocation kept for the life of the process.
+static uint32_t* persist_tickets(void* stream) {
+  static std::mutex mu;
+  static std::map<std::pair<int, void*>, uint32_t*> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = slots.find({dev, stream});
+  if (it != slots.end()) return it->second;
+  uint32_t* p = nullptr;
+  if (hipMalloc(&p, 2 * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, 2 * sizeof(uint32_t), reinterpret_cast<hipStream_t>(stream)) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  slots[{dev, stream}] = p;
+  return p;
+}
+
 // DDSP_HIP_PERSIST_LDSPAD=1: LDS per workgroup padded so that a CU holds at most wpc of them
 static size_t persist_lds_floor(int wpc) {
   static int pad = -1;
@@ -682,9 +796,11 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   const int64_t NF = batch * frames;
   const int cus = device_cus();
   const int wpc = persist_wgs_per_cu();
-  const int buf_floats = (int)((floats + 4 + 3) & ~(size_t)3);
+  const int buf_floats = (int)((floats + 8 + 3) & ~(size_t)3);
   const size_t pshm = sizeof(float) * 2 * (size_t)buf_floats;
-  if (G == 1 && wpc > 0 && cus > 0 && NF <= INT32_MAX && NF >= 2LL * cus * wpc && pshm <= 64 * 1024) {
+  uint32_t* tickets = nullptr;
+  if (G == 1 && wpc > 0 && cus > 0 && NF <= INT32_MAX && NF >= 2LL * cus * wpc && pshm <= 64 * 1024 &&
+      (tickets = persist_tickets(stream)) != nullptr) {
     const int pgrid = cus * wpc;
     const size_t lds = std::max(pshm, persist_lds_floor(wpc));
     const dim3 pblock((unsigned)(nt + 64));
@@ -692,7 +808,8 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
     hipLaunchKernelGGL((synth_persist_kernel<RNG_, CTRL_, kPersistPad<RNG_, CTRL_>>), dim3(pgrid), pblock, lds, \
                        S(stream), f0, param, raw_magnitudes, bias, RNG_ ? nullptr : noise, k0, k1, o0, o1,      \
                        RNG_ ? counter : nullptr, out, harmonic_out, noise_out, controls_out, (int)batch,          \
-                       (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats)
+                       (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats, \
+                       tickets)
     if (noise) {
       if (controls_out) DDSP_SYNTH_PERSIST_LAUNCH(false, true);
       else DDSP_SYNTH_PERSIST_LAUNCH(false, false);

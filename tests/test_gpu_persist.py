@@ -26,8 +26,8 @@ def dd():
 
 
 def _both(dd, fn):
-    """fn() with the persistent kernel (8 workgroups per CU) and with one workgroup per frame."""
-    prev = dd.core.set_persistent_workgroups(8)
+    """fn() with the persistent kernel (6 workgroups per CU) and with one workgroup per frame."""
+    prev = dd.core.set_persistent_workgroups(6)
     try:
         a = fn()
         dd.core.set_persistent_workgroups(0)
@@ -47,7 +47,7 @@ def _close(a, b, rel=2e-7):
 def test_persistent_matches_per_frame(dd, B, F, H, NB, bs):
     inp = make_inputs(B, F, H, NB, bs, seed=B + F, device="cuda")
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert B * F >= 2 * cus * 8 or bs == 1024, "shape must take the persistent kernel"
+    assert B * F >= 2 * cus * 6 or bs == 1024, "shape must take the persistent kernel"
 
     def run():
         with torch.no_grad():
@@ -71,7 +71,7 @@ def test_persistent_matches_per_frame(dd, B, F, H, NB, bs):
 
 def test_persistent_counter_replay(dd):
     """The device-counter entry point (graph replay) on the persistent kernel: call k draws offset k."""
-    dd.core.set_persistent_workgroups(8)
+    dd.core.set_persistent_workgroups(6)
     B, F, H, NB, bs = 24, 200, 40, 65, 512
     inp = make_inputs(B, F, H, NB, bs, seed=3, device="cuda", with_noise=False)
     counter = torch.zeros(1, dtype=torch.int64, device="cuda")
