@@ -25,6 +25,20 @@ namespace {
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The oscillator bank over the (k+1, amplitude) table for 4 samples: acc[s] += A_k sin(fl32(w_s (k+1)))
+// in ascending k.  H4 % 4 == 0.  (A register double buffer of the next 4 coefficients was re-rolled by
+// the compiler into load-then-use; forced through inline assembly it gained the compiler's own waits
+// and 11-15 extra instructions per iteration: not kept.)
+__device__ __forceinline__ void osc_bank4(const float2* __restrict__ coef, int H4, const float (&w)[4],
+                                          float (&acc)[4]) {
+#pragma unroll 4
+  for (int k = 0; k < H4; ++k) {
+    const float2 c = coef[k];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
+  }
+}
+
 // SPLIT (few-frame launches, e.g. the realtime stream's 4 frames per call): the workgroup has
 // G times the threads of one 4-samples-per-thread frame and the oscillator bank runs one sample
 // per thread, so one frame's latency is spread over G times the waves.
@@ -172,12 +186,7 @@ __device__ __forceinline__ bool frame_synth(
     if (active) {
 #endif
       if (fast) {
-#pragma unroll 4
-        for (int k = 0; k < H4; ++k) {
-          const float2 c = coef[k];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
-        }
+        osc_bank4(coef, H4, w, acc);
       } else {
         for (int k = 0; k < H; ++k) {
           const float2 c = coef[k];
@@ -646,12 +655,7 @@ __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
       if (false)
 #endif
       if (fast) {
-#pragma unroll 4
-        for (int k = 0; k < H4; ++k) {
-          const float2 c = coef[k];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc[s] = fmaf(sin_reduced(w[s] * c.x), c.y, acc[s]);
-        }
+        osc_bank4(coef, H4, w, acc);
       } else {
         for (int k = 0; k < H; ++k) {
           const float2 c = coef[k];
