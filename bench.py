@@ -387,27 +387,39 @@ def decoder_synthesis_leg(args, inp, dev, reps=50):
     synths with their controls, the sum, the returned parts and control dicts, the 1 s reverb) as the
     decoder runs it (decoder.decoder_synthesize, the fused kernel; install() binds the same function
     under the reference's DDSPDecoder.forward), from a fixed GRU output; device noise."""
-    from ddsp_pytorch_amd.decoder import DDSPDecoder, decoder_synthesize
+    from ddsp_pytorch_amd.decoder import DDSPDecoder, decoder_projections, decoder_synthesize
     B, F, bs = args.batch, args.frames, args.block_size
     torch.manual_seed(0)
     model = DDSPDecoder(512, args.harmonics, args.bands, args.sample_rate, bs, True).to(dev).eval()
     model.noise_synth.noise_mode = "device"
     if args.reverb_length != args.sample_rate:
         model.reverb = type(model.reverb)(args.reverb_length, args.sample_rate).to(dev)
-    with torch.no_grad():
-        hidden = model.decoder(inp["f0"], torch.randn(B, F, 1, device=dev))
-        run = lambda: decoder_synthesize(model, hidden, inp["f0"])
+    def timed(fn):
         for _ in range(10):
-            run()
+            fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            out = run()
+            r = fn()
         torch.cuda.synchronize()
-        t = (time.perf_counter() - t0) / reps
+        return (time.perf_counter() - t0) / reps, r
+
+    from ddsp_pytorch_amd import core
+    with torch.no_grad():
+        hidden = model.decoder(inp["f0"], torch.randn(B, F, 1, device=dev))
+        t, out = timed(lambda: decoder_synthesize(model, hidden, inp["f0"]))
+        t_proj, _ = timed(lambda: decoder_projections(model, hidden))
+        param, mags = decoder_projections(model, hidden)
+
+        def synth_rev():
+            sig = core.synth_frames(inp["f0"], param, mags, bs, args.sample_rate, parts=True, controls=True)[0]
+            return model.reverb(sig)
+        t_syn, _ = timed(synth_rev)
     assert torch.isfinite(out[0]).all()
     del model
     return {"value": round(B * F * bs / t, 1), "unit": "samples/s", "ms_per_step": round(t * 1e3, 4),
+            "split_ms": {"projections (one GEMM)": round(t_proj * 1e3, 4),
+                         "synthesis_parts_controls_reverb": round(t_syn * 1e3, 4)},
             "workload": f"decoder.py:106-125 synthesis section of DDSPDecoder(hidden 512, H {args.harmonics}, "
                         f"NB {args.bands}, reverb {args.reverb_length}) from a fixed GRU output: projections, "
                         "fused synthesis writing signal + harmonic + noise + control dicts, reverb; batch "

@@ -394,12 +394,22 @@ def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None
     return _synth_frames_launch(f0, param, mags, bs, sample_rate, bias, noise, parts, seed, offset, controls)
 
 
+def _frame_rows(t):
+    """(tensor, row stride) for a [B, F, C] tensor read row by row: unit stride on C and one row stride
+    over (B, F) — a column slice of a wider projection output qualifies as it is — else a contiguous copy."""
+    if t.dim() == 3 and t.stride(-1) == 1 and t.stride(0) == t.shape[1] * t.stride(1):
+        return t, t.stride(1)
+    t = t.contiguous()
+    return t, t.shape[-1]
+
+
 def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, parts, seed, offset,
                          controls=False):
     B, F, H1 = param.shape
     NB = mags.shape[-1]
     bs = int(block_size)
-    f0c, pc, mc = _c(f0), _c(param), _c(mags)
+    f0c = _c(f0)
+    (pc, ldp), (mc, ldm) = _frame_rows(param), _frame_rows(mags)
     if noise is not None:
         _dev(noise)
         if tuple(noise.shape) != (B, F, bs):
@@ -410,9 +420,9 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     nz = torch.empty_like(out) if parts else None
     ctrl = (torch.empty(B * F * (1 + (H1 - 1) + NB), dtype=torch.float32, device=f0.device)
             if controls else None)
-    _lib.call("synth_frames_controls", _lib.ptr(f0c), _lib.ptr(pc), _lib.ptr(mc), float(bias), _lib.ptr(noise),
-              seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), _lib.ptr(ctrl), B, F, H1 - 1, NB, bs,
-              float(sample_rate), _lib.stream_of(out))
+    _lib.call("synth_frames_controls", _lib.ptr(f0c), _lib.ptr(pc), ldp, _lib.ptr(mc), ldm, float(bias),
+              _lib.ptr(noise), seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), _lib.ptr(ctrl), B, F,
+              H1 - 1, NB, bs, float(sample_rate), _lib.stream_of(out))
     res = (out, harm, nz) if parts else out
     if not controls:
         return res

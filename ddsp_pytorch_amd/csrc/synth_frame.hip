@@ -56,7 +56,7 @@ __device__ __forceinline__ bool frame_synth(
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs,
     float sr, int lo_end, int tail_start, int pad, int f, int b, int tid, int NT, float4* smem4, double* red,
-    int w0, float (&acc)[4], float (&nz)[4], int& j0_out) {
+    int w0, float (&acc)[4], float (&nz)[4], int& j0_out, int ldp, int ldm) {
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
   float2* coef = reinterpret_cast<float2*>(smem4);       // [H4] (k+1, amplitude)
@@ -70,7 +70,7 @@ __device__ __forceinline__ bool frame_synth(
 
   const int64_t frame = (int64_t)b * F + f;
   const float* f0b = f0 + (int64_t)b * F;
-  const float* prow = param + frame * (H + 1);
+  const float* prow = param + frame * ldp;
   const float half_sr = sr * 0.5f;
   const float pitch0 = f0b[f];
 
@@ -85,7 +85,7 @@ __device__ __forceinline__ bool frame_synth(
     coef[k].y = v;
     part_d += (double)v;
   }
-  for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * NB + k] + bias);  // modules.py:113
+  for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * ldm + k] + bias);  // modules.py:113
   fill_cos_table(ct, n, tid, NT);
   for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
   const int quads = bs >> 2;
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
     float* __restrict__ noise_out, float* __restrict__ ctrl_out, int F, int H,
-    int NB, int bs, float sr, int lo_end, int tail_start, int pad) {
+    int NB, int bs, float sr, int lo_end, int tail_start, int pad, int ldp, int ldm) {
   extern __shared__ float4 smem4[];
   __shared__ double red[32];
   float acc[4], nz[4];
@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
 #endif
   if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
                                       (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
-                                      blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0))
+                                      blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0, ldp, ldm))
     return;
   const int64_t o = ((int64_t)blockIdx.y * F + blockIdx.x) * bs + j0;
 #ifdef DDSP_PROBE_CLOCK  // harm_out receives the probe: [compute ticks, store ticks, cycles, total ticks]
@@ -370,12 +370,12 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
                                            uint32_t off0, uint32_t off1, float* __restrict__ ctrl_out, int B,
                                            int F, int H, int NB, int bs, float sr, int lo_end, int tail_start,
                                            int pad, int frame, FrameBuf fb, int lane, bool carry,
-                                           double carry_S) {
+                                           double carry_S, int ldp, int ldm) {
   const int n = 2 * (NB - 1), half = n >> 1;
   const int H4 = (H + 3) & ~3;
   const int b = frame / F, f = frame - b * F;
   const float* f0b = f0 + (int64_t)b * F;
-  const float* prow = param + (int64_t)frame * (H + 1);
+  const float* prow = param + (int64_t)frame * ldp;
   const float half_sr = sr * 0.5f;
 #ifdef DDSP_PROBE_CLOCK
   uint64_t pts[6];
@@ -394,7 +394,7 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
   for (int r = 0; r < 2; ++r) {
     const int k = lane + 64 * r;
     pv[r] = k < H ? prow[1 + k] : 0.0f;
-    mv[r] = k < NB ? mags[(int64_t)frame * NB + k] : 0.0f;
+    mv[r] = k < NB ? mags[(int64_t)frame * ldm + k] : 0.0f;
   }
   const int quads = bs >> 2;
   // noise (modules.py:119-123): Philox while the loads are in flight, or the injected samples
@@ -443,7 +443,7 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
     fb.coef()[k].y = v;
     part_d += (double)v;
   }
-  for (int k = lane + 128; k < NB; k += 64) fb.A()[k] = scale_fn(mags[(int64_t)frame * NB + k] + bias);
+  for (int k = lane + 128; k < NB; k += 64) fb.A()[k] = scale_fn(mags[(int64_t)frame * ldm + k] + bias);
   const float norm = (float)wave_sum_double(part_d);  // dist.sum(-1)
   const float a = scale_fn(praw0);
   for (int k = lane; k < H4; k += 64) {  // each lane rereads only the values it wrote
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
     float* __restrict__ noise_out, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs, float sr,
-    int lo_end, int tail_start, int pad, int buf_floats, uint32_t* __restrict__ tickets) {
+    int lo_end, int tail_start, int pad, int buf_floats, uint32_t* __restrict__ tickets, int ldp, int ldm) {
   extern __shared__ float4 smem4[];
   const int NS = (int)blockDim.x - 64;  // synthesis threads; the last wave prepares
   const int tid = threadIdx.x;
@@ -611,7 +611,8 @@ __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
         if (probe_first < 0) probe_first = fr;
 #endif
         carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
-                                        bs, sr, lo_end, tail_start, pad, fr, nb, lane, fr == prev + 1, carry_S);
+                                        bs, sr, lo_end, tail_start, pad, fr, nb, lane, fr == prev + 1, carry_S, ldp,
+                                        ldm);
       }
       if (lane == 0) *nb.frame() = fr;
       __syncthreads();  // buffer i&1 prepared (or marked empty); the synthesis waves released the other one
@@ -763,8 +764,11 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
                                const float* noise, uint64_t seed, uint64_t offset, uint64_t* counter, float* out,
                                float* harmonic_out, float* noise_out, float* controls_out, int64_t batch, int64_t frames,
                                int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
-                               void* stream) {
+                               void* stream, int64_t param_ld = -1, int64_t mags_ld = -1) {
+  if (param_ld < 0) param_ld = n_harmonic + 1;
+  if (mags_ld < 0) mags_ld = n_bands;
   if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
+  if (param_ld < n_harmonic + 1 || mags_ld < n_bands || param_ld > INT32_MAX || mags_ld > INT32_MAX) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
   if (!f0 || !param || !raw_magnitudes || !out) return DDSP_HIP_EINVAL;
   // the fused kernel's shape envelope; callers fall back to the separate kernels outside it
@@ -813,7 +817,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
                        S(stream), f0, param, raw_magnitudes, bias, RNG_ ? nullptr : noise, k0, k1, o0, o1,      \
                        RNG_ ? counter : nullptr, out, harmonic_out, noise_out, controls_out, (int)batch,          \
                        (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats, \
-                       tickets)
+                       tickets, (int)param_ld, (int)mags_ld)
     if (noise) {
       if (controls_out) DDSP_SYNTH_PERSIST_LAUNCH(false, true);
       else DDSP_SYNTH_PERSIST_LAUNCH(false, false);
@@ -835,7 +839,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_, CTRL_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
                      bias, RNG_ ? nullptr : noise, k0, k1, o0, o1, RNG_ ? counter : nullptr, out, harmonic_out,  \
                      noise_out, controls_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, \
-                     tail_start, pad)
+                     tail_start, pad, (int)param_ld, (int)mags_ld)
   if (noise) {
     if (G > 1) DDSP_SYNTH_FRAME_LAUNCH(false, true);
     else DDSP_SYNTH_FRAME_LAUNCH(false, false);
@@ -862,14 +866,14 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                              noise_out, nullptr, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
 }
 
-int ddsp_hip_synth_frames_controls(const float* f0, const float* param, const float* raw_magnitudes, float bias,
-                                   const float* noise, uint64_t seed, uint64_t offset, float* out,
-                                   float* harmonic_out, float* noise_out, float* controls_out, int64_t batch,
-                                   int64_t frames, int64_t n_harmonic, int64_t n_bands, int64_t block_size,
-                                   float sample_rate, void* stream) {
+int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
+                                   int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed,
+                                   uint64_t offset, float* out, float* harmonic_out, float* noise_out,
+                                   float* controls_out, int64_t batch, int64_t frames, int64_t n_harmonic,
+                                   int64_t n_bands, int64_t block_size, float sample_rate, void* stream) {
   return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
                              noise_out, controls_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate,
-                             stream);
+                             stream, param_ld, magnitudes_ld);
 }
 
 int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const float* raw_magnitudes, float bias,

@@ -62,6 +62,30 @@ def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
     return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
 
 
+def decoder_projections(self, hidden):
+    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE GEMM over the
+    concatenated weights (the two outputs are column slices of it; the fused synthesis kernel reads them
+    with their row stride).  The concatenated weights are cached while the four parameters are unchanged
+    (keyed on their storage and version counters, like Reverb's spectrum)."""
+    hp, npj = self.harmonic_proj, self.noise_proj
+    if not hidden.is_cuda or hp.bias is None or npj.bias is None:
+        return hp(hidden), npj(hidden)
+    ps = (hp.weight, hp.bias, npj.weight, npj.bias)
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    cache = self.__dict__.get("_proj_cat")
+    if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
+        w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
+    elif cache is not None and cache[0] == key:
+        w, b = cache[1], cache[2]
+    else:
+        with torch.no_grad():
+            w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])
+        self.__dict__["_proj_cat"] = (key, w, b)
+    out = torch.nn.functional.linear(hidden, w, b)
+    h1 = hp.out_features
+    return out[..., :h1], out[..., h1:]
+
+
 def decoder_synthesize(self, hidden, f0):
     """decoder.py:106-125, the synthesis section of DDSPDecoder.forward: controls -> harmonic + noise
     (+ reverb).  On the fused kernel (one launch for both synths, their controls, the sum and the
@@ -71,8 +95,7 @@ def decoder_synthesize(self, hidden, f0):
     gfx950 kernels).  Works on this package's DDSPDecoder and, through install(), on the reference's.
     Returns (signal, harmonic, noise, harmonic_ctrls, noise_ctrls)."""
     hs, ns = self.harmonic_synth, self.noise_synth
-    param = self.harmonic_proj(hidden)
-    mags = self.noise_proj(hidden)
+    param, mags = decoder_projections(self, hidden)
     H, NB, bs = param.shape[-1] - 1, mags.shape[-1], int(hs.block_size)
     fused = (param.is_cuda and int(ns.block_size) == bs and param.shape[0] <= 65535
              and core.synth_frames_in_envelope(H, NB, bs, param.shape[0]))

@@ -152,12 +152,14 @@ int ddsp_hip_set_persistent_workgroups(int per_cu);
  * laid out as [amplitudes B*F | harmonic_distribution B*F*H | magnitudes B*F*NB]: amplitudes =
  * scale_function(param[...,0]), harmonic_distribution = the normalised distribution after
  * HarmonicSynth.forward's in-place `*= amplitudes` (modules.py:61,73), magnitudes =
- * scale_function(raw_magnitudes + bias) (modules.py:111-114). */
-int ddsp_hip_synth_frames_controls(const float* f0, const float* param, const float* raw_magnitudes, float bias,
-                                   const float* noise, uint64_t seed, uint64_t offset, float* out,
-                                   float* harmonic_out, float* noise_out, float* controls_out, int64_t batch,
-                                   int64_t frames, int64_t n_harmonic, int64_t n_bands, int64_t block_size,
-                                   float sample_rate, void* stream);
+ * scale_function(raw_magnitudes + bias) (modules.py:111-114).  param_ld / magnitudes_ld: elements between
+ * consecutive frames' rows (>= H + 1 / >= NB), so both may be column slices of one projection output
+ * (decoder.py:106-117 computed as a single GEMM). */
+int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
+                                   int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed,
+                                   uint64_t offset, float* out, float* harmonic_out, float* noise_out,
+                                   float* controls_out, int64_t batch, int64_t frames, int64_t n_harmonic,
+                                   int64_t n_bands, int64_t block_size, float sample_rate, void* stream);
 
 /* ddsp_hip_synth_frames for a stream of calls replayed from a captured HIP graph (the ddsp~
  * realtime host, realtime/ddsp_tilde/ddsp_model.cpp:32-52, calling the exported model once per

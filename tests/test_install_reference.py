@@ -130,7 +130,7 @@ def test_install_resolves_on_reference_instances():
         # every self.X it (and decoder_synthesize) reads exists on a reference DDSPDecoder, and the
         # attributes it reads off the synth modules too
         assert ref_decoder.DDSPDecoder.__dict__["forward"] is dd.decoder.decoder_forward
-        for fn in (dd.decoder.decoder_forward, dd.decoder.decoder_synthesize):
+        for fn in (dd.decoder.decoder_forward, dd.decoder.decoder_synthesize, dd.decoder.decoder_projections):
             missing = {a for a in _self_reads(fn) if not hasattr(model, a)}
             assert not missing, f"{fn.__name__} reads {missing}, absent on a reference DDSPDecoder"
         for attr in ("block_size", "sample_rate"):
