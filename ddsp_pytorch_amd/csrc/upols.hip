@@ -585,6 +585,10 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   if (nb > INT32_MAX || npairs > 65535) return DDSP_HIP_EINVAL;
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
+#ifdef DDSP_PROBE_REVERB_ONLY  // timing probe (tools/exp_cache.py): 1 forward only, 2 MAC + inverse only
+  if (DDSP_PROBE_REVERB_ONLY == 1) return launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
+  if (DDSP_PROBE_REVERB_ONLY == 2) return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
+#endif
   // Z_b = FFT([x_b, 0])
   int st = launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
   if (st) return st;
