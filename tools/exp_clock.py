@@ -80,11 +80,12 @@ def in_kernel():
         while time.perf_counter() - t < 0.3:
             body()
         torch.cuda.synchronize()
-        res = []
-        for _ in range(n):
+        res, runs = [], []
+        for _ in range(n):  # queued back to back; read after one synchronize
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            h = body(e0, e1)
-            torch.cuda.synchronize()
+            runs.append((e0, e1, body(e0, e1)))
+        torch.cuda.synchronize()
+        for e0, e1, h in runs:
             r = h[1].view(B * F, bs)[:, :6].double().cpu() / 100.0  # us (100 MHz ticks)
             start = r[:, 0] - r[:, 0].min()
             end = start + r[:, 3]
@@ -93,13 +94,13 @@ def in_kernel():
             bins = torch.arange(0, span + 1, 1.0, dtype=torch.float64)
             occ = ((start[None, :] <= bins[:, None]) & (end[None, :] > bins[:, None])).sum(1).double()
             res.append({"kernel": e0.elapsed_time(e1) * 1e3, "span": span,
-                        "clk": float(r[:, 5].sum() / r[:, 3].sum()),
+                        "clk": float(r[:, 5].sum() / r[:, 3].sum()) * 100.0, "clk_lo": float((r[:, 5] / r[:, 3]).quantile(0.05)) * 100.0, "clk_hi": float((r[:, 5] / r[:, 3]).quantile(0.95)) * 100.0,
                         "pro": float(r[:, 1].mean()), "osc": float((r[:, 2] - r[:, 1]).mean()),
                         "post": float((r[:, 4] - r[:, 2]).mean()), "store": float((r[:, 3] - r[:, 4]).mean()),
                         "occ_mean": float(occ.mean()), "occ": occ,
                         "first_end": float(end.min()), "last_start": float(start.max())})
         md = lambda k: statistics.median(x[k] for x in res)
-        print(f"{name:30s}: kernel {md('kernel'):6.1f} us (workgroup span {md('span'):6.1f}), SCLK {md('clk'):5.0f} MHz;"
+        print(f"{name:30s}: kernel {md('kernel'):6.1f} us (workgroup span {md('span'):6.1f}), SCLK {md('clk'):6.0f} MHz (5-95 % of workgroups {md('clk_lo'):5.0f}-{md('clk_hi'):5.0f});"
               f" workgroup life: prologue {md('pro'):5.2f} + sine loop {md('osc'):5.2f} + FIR/tail {md('post'):4.2f}"
               f" + store {md('store'):4.2f} us; resident workgroups mean {md('occ_mean'):6.0f} of 4096; first"
               f" end {md('first_end'):5.1f} us, last start {md('last_start'):6.1f} us", flush=True)

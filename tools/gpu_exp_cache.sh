@@ -1,2 +1,1 @@
-# does a small kernel between the reverb and the next synthesis launch remove the slowdown? (tools/exp_gap.py --reset)
-timeout -k 10 200 python tools/exp_gap.py --reset > gpurun_out/exp_gap2.log 2>&1
+DDSP_HIP_LIB=$PWD/build/ab_clk.so timeout -k 10 300 python tools/exp_clock.py --in-kernel > gpurun_out/exp_clock_ik3.log 2>&1
