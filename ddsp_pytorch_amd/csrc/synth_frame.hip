@@ -19,6 +19,8 @@
 
 #include "common.h"
 #include "noise_dsp.h"
+#include "fft_radix.h"
+#include "upols.h"
 
 namespace ddsp {
 namespace {
@@ -698,9 +700,126 @@ __global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
 
 using namespace ddsp;
 
+// sine-loop placement padding of the fused synthesis + forward-transform instantiations (tools/loop_align.py)
+template <bool RNG>
+constexpr bool kSynthForwardPad = false;
+
 // sine-loop placement padding of the persistent instantiations (tools/loop_align.py)
 template <bool RNG, bool CTRL>
 constexpr bool kPersistPad = false;
+
+
+namespace ddsp {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Synthesis fused with the reverb's forward transform (decoder.py:106-125: the synthesis section
+// and Reverb.forward's first step, modules.py:28-35 via upols.hip).  The reverb's partitioned
+// convolution starts from Z_b = FFT_4096([x_b, 0]) of every 2048-sample block of two packed rows
+// (x_a + i x_b); here one workgroup per (pair of rows, block) synthesises the block's 2 x (2048/bs)
+// frames — a thread group of NT threads per frame, exactly frame_synth as in synth_frame_kernel —
+// and transforms them in LDS, so the dry signal never goes to HBM (26 MB written and re-read at
+// config 2) and the forward transform's launch disappears.  The transform: four radix-8 Stockham
+// passes by 512 threads (8 points each: the frame buffers' 64-VGPR budget, which the separate
+// forward kernel's 16-point radix-16 passes exceed), its buffer overlaying the frame buffers.
+// Z is the layout upols_apply_spectra reads ([pair][block][4096]); the MAC and inverse follow.
+struct Tw3 {
+  float2 w1, w2, w4;
+};
+template <bool INV>
+__device__ __forceinline__ Tw3 radix8_tw(int step) {
+  return Tw3{twiddle(step, INV), twiddle(2 * step, INV), twiddle(4 * step, INV)};
+}
+__device__ __forceinline__ void radix8_twiddle(float2 (&v)[8], const Tw3& t) {
+  const float2 w1 = t.w1, w2 = t.w2, w4 = t.w4;
+  const float2 w3 = cmul(w1, w2);
+  v[1] = cmul(v[1], w1);
+  v[2] = cmul(v[2], w2);
+  v[3] = cmul(v[3], w3);
+  v[4] = cmul(v[4], w4);
+  v[5] = cmul(v[5], cmul(w4, w1));
+  v[6] = cmul(v[6], cmul(w4, w2));
+  v[7] = cmul(v[7], cmul(w4, w3));
+}
+
+template <bool RNG, bool PAD>
+__global__ void __launch_bounds__(1024, 8) synth_forward_kernel(
+    const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
+    float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
+    const uint64_t* __restrict__ counter, float2* __restrict__ Z, int B, int F, int H, int NB, int bs,
+    float sr, int lo_end, int tail_start, int pad, int gfloats, int NT, int nb, int ldp, int ldm) {
+  extern __shared__ float4 smem4[];
+  __shared__ double red[32];
+  const int fpb = kP / bs;  // frames per block
+  const int g = threadIdx.x / NT, tid = threadIdx.x - g * NT;
+  const int rr = g / fpb, fl = g - rr * fpb;  // row of the pair, frame of the block
+  const int blk = blockIdx.x, pair = blockIdx.y;
+  const int row = 2 * pair + rr, f = blk * fpb + fl;
+  const bool valid = row < B && f < F;  // else zeros (an odd batch's missing row, frames past T)
+  float acc[4], nz[4];
+  int j0;
+  // groups outside the signal synthesise a clamped frame (every group runs frame_synth's barriers)
+  const bool act = frame_synth<RNG, false, PAD, false>(
+      f0, param, mags, bias, noise, k0, k1, off0, off1, counter, nullptr, B, F, H, NB, bs, sr, lo_end, tail_start,
+      pad, min(f, F - 1), min(row, B - 1), tid, NT, smem4 + (size_t)g * (gfloats >> 2), red, g * (NT >> 6), acc, nz,
+      j0, ldp, ldm);
+#ifdef DDSP_PROBE_SR_NOFFT  // timing probe: the synthesis alone at this launch shape (tools/exp_synth_reverb.py)
+  if (act && acc[0] + nz[0] == 1234.5f) Z[threadIdx.x] = make_float2(acc[1], nz[1]);
+  return;
+#endif
+  __syncthreads();  // every frame buffer is free: the transform buffer overlays them
+  float2* buf = reinterpret_cast<float2*>(smem4);
+  float* bf = reinterpret_cast<float*>(smem4);
+  if (act) {
+    const int p0 = fl * bs + j0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bf[2 * lds_idx(p0 + s) + rr] = valid ? acc[s] + nz[s] : 0.0f;  // decoder.py:121
+  }
+  __syncthreads();
+  constexpr int NTF = kN / 8;  // transform threads
+  if (threadIdx.x < NTF) {
+    const int j = threadIdx.x;
+    // the passes' twiddles first: their loads' latency hides behind the first pass
+    Tw3 tw[3];
+#pragma unroll
+    for (int pass = 1; pass < 4; ++pass) {
+      const int ns = 1 << (3 * pass);
+      tw[pass - 1] = radix8_tw<false>((j & (ns - 1)) * (kN / 8 / ns));
+    }
+    float2 v[8];
+    // pass 1 (Ns = 1): inputs j + 512 r; r >= 4 is the block's zero half
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = buf[lds_idx(j + NTF * r)];
+#pragma unroll
+    for (int r = 4; r < 8; ++r) v[r] = make_float2(0.0f, 0.0f);
+    dft8<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    int Ns = 1;
+#pragma unroll
+    for (int pass = 1; pass < 4; ++pass) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) buf[lds_idx((j / Ns) * Ns * 8 + (j & (Ns - 1)) + r * Ns)] = v[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = buf[lds_idx(j + NTF * r)];
+      Ns *= 8;
+      radix8_twiddle(v, tw[pass - 1]);
+      dft8<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    }
+    float2* out = Z + ((int64_t)pair * nb + blk) * kN;  // Ns = 512: natural order j + 512 r
+#pragma unroll
+    for (int r = 0; r < 8; ++r) out[j + NTF * r] = v[r];
+  } else {
+#pragma unroll
+    for (int pass = 1; pass < 4; ++pass) {
+      __syncthreads();
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+}  // namespace ddsp
 
 // compute units of the current device (cached per device)
 static int device_cus() {
@@ -758,6 +877,33 @@ static size_t persist_lds_floor(int wpc) {
   return pad && wpc > 0 ? (size_t)(160 * 1024 / (wpc + 1) + 1024) : 0;
 }
 
+// a frame's LDS layout (frame_synth): the FIR's first run [0, lo_end) and the wrapped taps from
+// tail_start, the zero padding ahead of the samples, and the floats of one frame buffer
+struct FrameShape {
+  int lo_end, tail_start, pad;
+  size_t floats;
+};
+static FrameShape frame_shape(int64_t n_harmonic, int64_t n_bands, int bs) {
+  const int n = 2 * (int)(n_bands - 1), half = n / 2;
+  FrameShape fs;
+  if (bs >= n) {
+    fs.lo_end = (half + 3) & ~3;
+    fs.tail_start = bs - half;
+    if (fs.tail_start < fs.lo_end) {
+      fs.lo_end = bs;
+      fs.tail_start = bs;
+    }
+  } else {
+    fs.lo_end = bs;
+    fs.tail_start = bs;
+  }
+  fs.pad = (fs.lo_end + 4 + 3) & ~3;
+  const int H4 = ((int)n_harmonic + 3) & ~3, n4 = (n + 3) & ~3;
+  fs.floats = (size_t)2 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs + ((half + 3) & ~3) +
+              fs.pad + bs;
+  return fs;
+}
+
 extern "C" {
 
 static int synth_frames_launch(const float* f0, const float* param, const float* raw_magnitudes, float bias,
@@ -775,23 +921,10 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   if (block_size % 4 || block_size > 1024 || n_harmonic > 1024 || n_bands > 1025 || batch > 65535 ||
       frames > INT32_MAX)
     return DDSP_HIP_ERANGE;
-  const int n = 2 * (int)(n_bands - 1), half = n / 2, bs = (int)block_size;
-  int lo_end, tail_start;
-  if (bs >= n) {
-    lo_end = (half + 3) & ~3;
-    tail_start = bs - half;
-    if (tail_start < lo_end) {
-      lo_end = bs;
-      tail_start = bs;
-    }
-  } else {
-    lo_end = bs;
-    tail_start = bs;
-  }
-  const int pad = (lo_end + 4 + 3) & ~3;
-  const int H4 = ((int)n_harmonic + 3) & ~3, n4 = (n + 3) & ~3;
-  const size_t floats = (size_t)2 * H4 + n4 + (((int)n_bands + 3) & ~3) + ((half + 4) & ~3) + bs +
-                        ((half + 3) & ~3) + pad + bs;
+  const int bs = (int)block_size;
+  const FrameShape fs = frame_shape(n_harmonic, n_bands, bs);
+  const int lo_end = fs.lo_end, tail_start = fs.tail_start, pad = fs.pad;
+  const size_t floats = fs.floats;
   if (sizeof(float) * floats > 120 * 1024) return DDSP_HIP_ERANGE;
   const int nt = std::max(64, ((bs / 4 + 63) / 64) * 64);
   // few frames (far fewer workgroups than CUs): split each frame's harmonics over G thread groups
@@ -883,6 +1016,72 @@ int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const flo
   if (!counter) return DDSP_HIP_EINVAL;
   return synth_frames_launch(f0, param, raw_magnitudes, bias, nullptr, seed, 0, counter, out, nullptr, nullptr,
                              nullptr, batch, frames, n_harmonic, n_bands, block_size, sample_rate, stream);
+}
+
+size_t ddsp_hip_synth_reverb_workspace_size(int64_t batch, int64_t frames, int64_t block_size) {
+  if (batch < 1 || frames < 1 || block_size < 1) return 0;
+  return upols_workspace_bytes(batch, frames * block_size, true);
+}
+
+int ddsp_hip_synth_reverb_spectra(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
+                                  int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed, uint64_t offset,
+                                  float* spectra, size_t spectra_bytes, int64_t batch, int64_t frames,
+                                  int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                                  void* stream) {
+  if (param_ld < 0) param_ld = n_harmonic + 1;
+  if (magnitudes_ld < 0) magnitudes_ld = n_bands;
+  if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
+  if (param_ld < n_harmonic + 1 || magnitudes_ld < n_bands || param_ld > INT32_MAX || magnitudes_ld > INT32_MAX)
+    return DDSP_HIP_EINVAL;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
+  if (!f0 || !param || !raw_magnitudes || !spectra) return DDSP_HIP_EINVAL;
+  // envelope: whole frames per 2048-sample block, one 64..256-thread group per frame, 2 rows x
+  // (2048 / bs) groups of at least the transform's 512 threads and at most 1024
+  const int bs = (int)block_size;
+  if (bs % 4 || kP % bs || n_harmonic > 1024 || n_bands > 1025 || batch > 2 * 65535 || frames > INT32_MAX)
+    return DDSP_HIP_ERANGE;
+  const int NT = std::max(64, ((bs / 4 + 63) / 64) * 64);
+  const int threads = 2 * (kP / bs) * NT;
+  if (threads < kN / 8 || threads > 1024) return DDSP_HIP_ERANGE;
+  const FrameShape fs = frame_shape(n_harmonic, n_bands, bs);
+  const int gfloats = (int)((fs.floats + 3) & ~(size_t)3);
+  const size_t shm = std::max(sizeof(float) * (size_t)gfloats * (threads / NT), sizeof(float2) * (kN + kN / 16));
+  if (shm > 160 * 1024) return DDSP_HIP_ERANGE;
+  const int64_t n = frames * block_size;
+  const int64_t nb = upols_blocks(n), npairs = (batch + 1) / 2;
+  if (nb > INT32_MAX) return DDSP_HIP_ERANGE;
+  if (spectra_bytes < upols_spectra_bytes(batch, n)) return DDSP_HIP_EWORKSPACE;
+  float2* Z = reinterpret_cast<float2*>(spectra);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
+#define DDSP_SYNTH_FORWARD_LAUNCH(RNG_)                                                                        \
+  hipLaunchKernelGGL((synth_forward_kernel<RNG_, kSynthForwardPad<RNG_>>), dim3((unsigned)nb, (unsigned)npairs),     \
+                     dim3(threads), shm, S(stream), f0, param, raw_magnitudes, bias, RNG_ ? nullptr : noise, k0, k1, \
+                     o0, o1, nullptr, Z, (int)batch, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate,    \
+                     fs.lo_end, fs.tail_start, fs.pad, gfloats, NT, (int)nb, (int)param_ld, (int)magnitudes_ld)
+  if (noise) DDSP_SYNTH_FORWARD_LAUNCH(false);
+  else DDSP_SYNTH_FORWARD_LAUNCH(true);
+#undef DDSP_SYNTH_FORWARD_LAUNCH
+  return launch_status();
+}
+
+int ddsp_hip_synth_reverb(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
+                          int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed, uint64_t offset,
+                          const float* spectrum, int64_t ir_length, float* out, void* workspace,
+                          size_t workspace_bytes, int64_t batch, int64_t frames, int64_t n_harmonic, int64_t n_bands,
+                          int64_t block_size, float sample_rate, void* stream) {
+  if (batch < 0 || frames < 0 || block_size < 4 || ir_length < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
+  if (!spectrum || !out) return DDSP_HIP_EINVAL;
+  const int64_t n = frames * block_size;
+  if (!workspace || workspace_bytes < upols_workspace_bytes(batch, n, true)) return DDSP_HIP_EWORKSPACE;
+  const size_t zb = upols_spectra_bytes(batch, n);
+  int st = ddsp_hip_synth_reverb_spectra(f0, param, param_ld, raw_magnitudes, magnitudes_ld, bias, noise, seed, offset,
+                                         reinterpret_cast<float*>(workspace), zb, batch, frames, n_harmonic, n_bands,
+                                         block_size, sample_rate, stream);
+  if (st) return st;
+  return upols_apply_spectra(reinterpret_cast<const float2*>(workspace), batch, n, spectrum, std::min(ir_length, n),
+                             false, out, reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) + zb), stream);
 }
 
 }  // extern "C"
