@@ -670,9 +670,10 @@ def main():
         "roofline": roofline,
         "op_boundary_effective": op_boundary_effective,
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
-        "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region "
-                          "(the VALU-bound synthesis kernel runs up to ~20% slower once the device "
-                          "is hot; roofline.avg_launch_ms is from inside the timed region)",
+        "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region; "
+                          "roofline.avg_launch_ms is from inside it.  The synthesis kernel's time depends "
+                          "on what ran before it: after the reverb (the step's order) the chip runs it at "
+                          "~2.2 instead of ~2.38 GHz (in-kernel clock probe, DESIGN.md 3c)",
     }
 
     if syn.reverb is not None and not args.no_uncached_leg:

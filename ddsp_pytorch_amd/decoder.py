@@ -62,14 +62,22 @@ def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
     return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
 
 
+def _hooked(m):
+    """A module call that must stay a module call: forward (pre-)hooks registered on it or globally, or
+    a subclass / wrapper whose forward is not nn.Linear's."""
+    from torch.nn.modules import module as _m
+    return bool(m._forward_hooks or m._forward_pre_hooks or _m._global_forward_hooks or
+                _m._global_forward_pre_hooks or type(m).forward is not torch.nn.Linear.forward)
+
+
 def decoder_projections(self, hidden):
     """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE GEMM over the
     concatenated weights (the two outputs are column slices of it; the fused synthesis kernel reads them
     with their row stride).  The concatenated weights are cached while the four parameters are unchanged
     (keyed on their storage and version counters, like Reverb's spectrum)."""
     hp, npj = self.harmonic_proj, self.noise_proj
-    if not hidden.is_cuda or hp.bias is None or npj.bias is None:
-        return hp(hidden), npj(hidden)
+    if not hidden.is_cuda or hp.bias is None or npj.bias is None or _hooked(hp) or _hooked(npj):
+        return hp(hidden), npj(hidden)  # (module hooks see the calls the reference makes)
     ps = (hp.weight, hp.bias, npj.weight, npj.bias)
     key = tuple((p.data_ptr(), p._version) for p in ps)
     cache = self.__dict__.get("_proj_cat")

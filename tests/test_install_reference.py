@@ -155,3 +155,22 @@ def test_install_resolves_on_reference_instances():
         assert getattr(ddsp, n) is f
     assert ref_decoder.GRUDecoder.__dict__["forward"] is orig_gru
     assert ref_decoder.DDSPDecoder.__dict__["forward"] is orig_dec
+
+
+def test_projection_hooks_keep_module_calls():
+    """decoder_projections runs the two projections as one GEMM only while nothing observes the
+    module calls: a forward hook (or a Linear subclass) keeps harmonic_proj/noise_proj as calls."""
+    import torch
+    from ddsp_pytorch_amd.decoder import _hooked
+    lin = torch.nn.Linear(4, 3)
+    assert not _hooked(lin)
+    h = lin.register_forward_hook(lambda m, i, o: None)
+    assert _hooked(lin)
+    h.remove()
+    assert not _hooked(lin)
+
+    class Wrapped(torch.nn.Linear):
+        def forward(self, x):
+            return super().forward(x) * 2
+
+    assert _hooked(Wrapped(4, 3))
