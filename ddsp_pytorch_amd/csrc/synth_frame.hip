@@ -280,7 +280,10 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
 #ifdef DDSP_PROBE_CLOCK  // shader clocks and 100 MHz ticks over the workgroup's life (tools/exp_clock.py)
   const uint64_t pc0 = clock64(), pt0 = wall_clock64();
 #endif
-  if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
+#ifndef DDSP_PAD_XOR  // A/B builds: -DDDSP_PAD_XOR=1 flips every instantiation's sine-loop padding
+#define DDSP_PAD_XOR 0
+#endif
+  if (!frame_synth<RNG, SPLIT, /*PAD=*/(CTRL != (bool)DDSP_PAD_XOR), CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
                                       (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
                                       blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0, ldp, ldm))
     return;

@@ -1,2 +1,2 @@
-timeout -k 10 300 python -u -m pytest tests/test_gpu_synth_reverb.py -x -q --timeout 120 --timeout-method thread > gpurun_out/sr_tests.log 2>&1; tail -1 gpurun_out/sr_tests.log
-timeout -k 10 200 python tools/exp_synth_reverb.py > gpurun_out/exp_sr2.log 2>&1
+# oscillator encodings A/B (tools/ab_build.sh variants of synth_frame.hip)
+for v in cur rndnep vconst vconstp rndlit cur; do echo "== $v" >> gpurun_out/exp_enc.log; DDSP_HIP_LIB=$PWD/build/ab_$v.so timeout -k 10 200 python tools/exp_timing.py --short >> gpurun_out/exp_enc.log 2>&1 || exit 1; done
