@@ -30,22 +30,19 @@ def shard(t, rank, world):
 def gather_audio(local, batch, dst=0, group=None):
     """Collect every rank's [b_i, T, 1] shard into [batch, T, 1] on rank ``dst`` (None elsewhere).
 
-    Shards may be ragged (batch % world != 0): each is padded to the largest shard for the
-    collective and trimmed on the root."""
-    world = dist.get_world_size(group)
+    Equal shards are received straight into the [batch, T, 1] result (its row blocks); ragged
+    shards (batch % world != 0) are padded to the largest shard for the collective and trimmed on
+    the root."""
     rank = dist.get_rank(group)
-    sizes = [shard_range(batch, r, world) for r in range(world)]
-    width = max(b - a for a, b in sizes)
-    send = local
-    if local.shape[0] < width:
-        pad = torch.zeros((width - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                          device=local.device)
-        send = torch.cat([local, pad], 0)
-    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
-    dist.gather(send.contiguous(), recv, dst=dst, group=group)
+    result = local.new_empty((batch,) + tuple(local.shape[1:])) if rank == dst else None
+    work, recv, sizes = _gather_async(local, batch, dst, group, into=result)
+    work.wait()
     if rank != dst:
         return None
-    return torch.cat([r[: b - a] for r, (a, b) in zip(recv, sizes)], 0)
+    if recv is not None:
+        for r, (a, b) in zip(recv, sizes):
+            result[a:b].copy_(r[: b - a])
+    return result
 
 
 def synthesize_sharded(synth, inputs, rank, world, gather=False, dst=0):
@@ -119,7 +116,10 @@ def _scatter_async(full, batch, width_cols, dtype, device, src, group):
     return work, recv, b - a
 
 
-def _gather_async(local, batch, dst, group):
+def _gather_async(local, batch, dst, group, into=None):
+    """Start gathering the ragged shards [b_r, ...] of a ``batch``-item chunk on dst.  With ``into``
+    (dst's [batch, ...] destination) and equal shards, the receive buffers are its row blocks, so
+    the result needs no copy; ragged shards are padded to the widest and compacted afterwards."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = [shard_range(batch, r, world) for r in range(world)]
@@ -127,9 +127,15 @@ def _gather_async(local, batch, dst, group):
     send = local
     if local.shape[0] < width:
         send = torch.cat([local, local.new_zeros((width - local.shape[0],) + tuple(local.shape[1:]))], 0)
-    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    direct = into is not None and all(b - a == width for a, b in sizes)
+    if rank != dst:
+        recv = None
+    elif direct:
+        recv = [into[a:b] for a, b in sizes]  # contiguous row blocks of the destination
+    else:
+        recv = [torch.empty_like(send) for _ in range(world)]
     work = dist.gather(send.contiguous(), recv, dst=dst, group=group, async_op=True)
-    return work, recv, sizes
+    return work, (None if direct else recv), sizes
 
 
 def chunk_bounds(batch, chunks):
@@ -162,16 +168,20 @@ def synthesize_pipelined(synth, inputs, batch, tails, chunks=4, src=0, dst=0, gr
 
     pending = start(0)
     gathers = []
+    result = None
     for c in range(len(bounds)):
         work, recv, n = pending
         work.wait()
         if c + 1 < len(bounds):
             pending = start(c + 1)  # in flight while this chunk is synthesised
         audio = synth(*unpack_items(recv[:n], tails))
-        gathers.append(_gather_async(audio, bounds[c][1] - bounds[c][0], dst, group))
-    out = []
-    for work, recv, sizes in gathers:
+        a, b = bounds[c]
+        if rank == dst and result is None:  # every rank's audio has this item shape
+            result = audio.new_empty((batch,) + tuple(audio.shape[1:]))
+        gathers.append((a, _gather_async(audio, b - a, dst, group, into=result[a:b] if result is not None else None)))
+    for a, (work, recv, sizes) in gathers:
         work.wait()
-        if rank == dst:
-            out.append(torch.cat([r[: b - a] for r, (a, b) in zip(recv, sizes)], 0))
-    return torch.cat(out, 0) if rank == dst else None
+        if rank == dst and recv is not None:  # ragged shards: compact the padded blocks
+            for r, (s0, s1) in zip(recv, sizes):
+                result[a + s0:a + s1].copy_(r[: s1 - s0])
+    return result if rank == dst else None
