@@ -338,6 +338,7 @@ def _filtered_noise_launch(magnitudes, block_size, noise, add, return_noise, raw
     return (out, nout) if nout is not None else out
 
 
+EWORKSPACE = 4  # DDSP_HIP_EWORKSPACE
 ERANGE = 5
 
 

@@ -98,3 +98,27 @@ def test_synth_path_fused_route():
         fused = syn(inp["f0"], inp["param"], inp["mags"], inp["noise"])
     torch.cuda.synchronize()
     assert float((fused - ref).abs().max()) < 2e-5
+
+
+def test_one_call_c_entry_matches_halves():
+    """ddsp_hip_synth_reverb (one C call: spectra + reverb in the caller's workspace) equals
+    synth_reverb_spectra + reverb_apply_spectra; bad workspace sizes are refused."""
+    from ddsp_pytorch_amd import _lib, core
+    with torch.no_grad():
+        inp, syn = _setup(4, 24, 512, L=4800, seed=4)
+        B, F, bs = 4, 24, 512
+        T = F * bs
+        spec = syn.reverb._spectrum(T)
+        ref = _fused(inp, syn, inp["noise"])
+        out = torch.empty(B, T, 1, device="cuda")
+        need = int(_lib.query("synth_reverb_workspace_size", B, F, bs))
+        ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+        p, m = inp["param"].contiguous(), inp["mags"].contiguous()
+        args = lambda nbytes: (_lib.ptr(inp["f0"].contiguous()), _lib.ptr(p), p.shape[-1], _lib.ptr(m), m.shape[-1],
+                               -5.0, _lib.ptr(inp["noise"].contiguous()), 0, 0, _lib.ptr(spec), syn.reverb.length,
+                               _lib.ptr(out), _lib.ptr(ws), nbytes, B, F, p.shape[-1] - 1, m.shape[-1], bs, 48000.0,
+                               _lib.stream_of(out))
+        assert _lib.call("synth_reverb", *args(need - 1), allow=(core.EWORKSPACE,)) == core.EWORKSPACE
+        _lib.call("synth_reverb", *args(need))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

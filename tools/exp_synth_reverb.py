@@ -23,6 +23,11 @@ def main():
     two = lambda: core.reverb_apply(core.synth_frames(inp["f0"], inp["param"], inp["mags"], bs, sr), spec, 48000)
     fused = lambda: core.synth_reverb(inp["f0"], inp["param"], inp["mags"], bs, sr, spec, 48000)
     E = lambda: torch.cuda.Event(enable_timing=True)
+    if "--fused-only" in sys.argv:  # a short run for rocprofv3 --pmc passes
+        for _ in range(20):
+            fused()
+        torch.cuda.synchronize()
+        return
 
     def group(fn, n=50, reps=7):
         t = time.perf_counter()
