@@ -135,8 +135,15 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
 #ifdef DDSP_PROBE_FWD_NOSTORE
   if (v[3].x == 1234.5f)
 #endif
+#ifdef DDSP_FWD_NT  // A/B: streaming (non-temporal) stores of the spectra
+  typedef float f2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    __builtin_nontemporal_store((f2v){v[r].x, v[r].y}, reinterpret_cast<f2v*>(out + j + 256 * r));
+#else
 #pragma unroll
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+#endif
 }
 
 // 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
@@ -144,10 +151,11 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
 // wave-uniform, so the descriptor lives in SGPRs.
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 constexpr int kBufferWord3 = 0x00020000;  // gfx9 raw-buffer DATA_FORMAT word
+template <int AUX = 0>  // cache-policy bits of the load (gfx950: 1 sc0, 2 nt, 16 sc1)
 __device__ __forceinline__ float2 row_load(const float2* row, int bytes, int voff) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(row), (short)0, bytes, kBufferWord3);
-  const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, AUX);
   return make_float2(__int_as_float(v.x), __int_as_float(v.y));
 }
 
@@ -213,9 +221,15 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
     win[0] = bn >= 0 ? xv : zero;
   }
   float2* Yp = Y + (int64_t)pair * nb * kN + f;
+#ifdef DDSP_MAC_YNT  // A/B: streaming stores of Y
+#pragma unroll
+  for (int d = 0; d < BLK; ++d)
+    if (b0 + d >= 0) __builtin_nontemporal_store(acc[d], reinterpret_cast<v2f*>(Yp + (int64_t)(b0 + d) * kN));
+#else
 #pragma unroll
   for (int d = 0; d < BLK; ++d)
     if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
+#endif
 }
 
 // The same sums with the Z window as a register ring indexed statically.  The p loop is unrolled by
@@ -246,8 +260,23 @@ __global__ void __launch_bounds__(kNT, UPOLS_RING_WAVES) upols_mac_ring_kernel(c
   const int voff = f * (int)sizeof(float2);
   float2 ring[R], g[GR];
   v2f acc[BLK];
-  auto zload = [&](int m, float2& dst) { dst = row_load(Xrow + (int64_t)max(m, 0) * kN, m >= 0 ? kRow : 0, voff); };
-  auto gload = [&](int q, float2& dst) { dst = row_load(Hrow + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+// Cache policy of the input-spectra (Z) and kernel-spectra (G) loads: non-temporal (nt; G also
+// sc0).  With the default policy the fused synthesis kernel that follows the reverb in the next
+// step runs at ~2.2 instead of ~2.38 GHz: the G loads' nt bit removes that, the Z
+// loads' adds a little (config-2 step 223.8-226.3 -> 208.3 us, tools/exp_timing.py, same box).
+// A/B builds override them (-DDDSP_MAC_ZAUX=0 -DDDSP_MAC_GAUX=0: the round-2 policy).
+#ifndef DDSP_MAC_ZAUX
+#define DDSP_MAC_ZAUX 2
+#endif
+#ifndef DDSP_MAC_GAUX
+#define DDSP_MAC_GAUX 3
+#endif
+  auto zload = [&](int m, float2& dst) {
+    dst = row_load<DDSP_MAC_ZAUX>(Xrow + (int64_t)max(m, 0) * kN, m >= 0 ? kRow : 0, voff);
+  };
+  auto gload = [&](int q, float2& dst) {
+    dst = row_load<DDSP_MAC_GAUX>(Hrow + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff);
+  };
 #pragma unroll
   for (int d = 0; d < BLK; ++d) {
     acc[d] = (v2f){0.f, 0.f};
@@ -287,8 +316,17 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
   const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
   const float2* in = Y + ((int64_t)pair * nb + b) * kN;
   float2 v[16];
+#ifdef DDSP_INV_NT  // A/B: streaming loads of Y
+  typedef float f2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(in + j + 256 * r));
+    v[r] = make_float2(t.x, t.y);
+  }
+#else
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = in[j + 256 * r];
+#endif
   fft4096<true>(v, lds);
   int ra, rb;
   pair_rows(pair, rows, pairing, ra, rb);
@@ -585,9 +623,22 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   if (nb > INT32_MAX || npairs > 65535) return DDSP_HIP_EINVAL;
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
-#ifdef DDSP_PROBE_REVERB_ONLY  // timing probe (tools/exp_cache.py): 1 forward only, 2 MAC + inverse only
-  if (DDSP_PROBE_REVERB_ONLY == 1) return launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
-  if (DDSP_PROBE_REVERB_ONLY == 2) return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
+#ifdef DDSP_PROBE_REVERB_ONLY  // timing probe (tools/exp_cache.py, exp_gap.py): a subset of the reverb's kernels
+  // 1 forward, 2 MAC + inverse, 3 forward + MAC, 4 forward + inverse, 5 MAC, 6 inverse,
+  // 7 forward into the Y buffer + MAC from the (stale) X: both kernels, no fresh data between them
+  constexpr int PR = DDSP_PROBE_REVERB_ONLY;
+  if (PR == 1 || PR == 3 || PR == 4) launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
+  if (PR == 7) launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, Y, stream);
+  if (PR == 2) return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
+  if (PR == 3 || PR == 5 || PR == 7)
+    hipLaunchKernelGGL((upols_mac_ring_kernel<UPOLS_RING_BLK, UPOLS_RING_PF, UPOLS_RING_GR>),
+                       dim3(kN / kNT, (unsigned)((nb + UPOLS_RING_BLK - 1) / UPOLS_RING_BLK), (unsigned)npairs), dim3(kNT),
+                       0, S(stream), X, reinterpret_cast<const float2*>(spectrum), (int64_t)0, (int)nb,
+                       (int)upols_kernel_windows(std::min(klen, n)), Y);
+  if (PR == 4 || PR == 6)
+    hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), Y, (int)nb,
+                       n, (int)rows, (int)pairing, (int)reverse, y, n);
+  return launch_status();
 #endif
   // Z_b = FFT([x_b, 0])
   int st = launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
