@@ -467,8 +467,18 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* _
   const int voff = f * (int)sizeof(float2);
   float2 ring[R], g[GR];
   v2f acc[BLK];
-  auto zload = [&](int m, float2& dst) { dst = row_load(Grow + (int64_t)min(m, nb - 1) * kN, m < nb ? kRow : 0, voff); };
-  auto hload = [&](int q, float2& dst) { dst = row_load(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+#ifndef DDSP_ADJ_ZAUX  // A/B: cache policy of the adjoint MAC's loads (as DDSP_MAC_ZAUX / _GAUX)
+#define DDSP_ADJ_ZAUX 0
+#endif
+#ifndef DDSP_ADJ_HAUX
+#define DDSP_ADJ_HAUX 0
+#endif
+  auto zload = [&](int m, float2& dst) {
+    dst = row_load<DDSP_ADJ_ZAUX>(Grow + (int64_t)min(m, nb - 1) * kN, m < nb ? kRow : 0, voff);
+  };
+  auto hload = [&](int q, float2& dst) {
+    dst = row_load<DDSP_ADJ_HAUX>(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff);
+  };
 #pragma unroll
   for (int d = 0; d < BLK; ++d) {
     acc[d] = (v2f){0.f, 0.f};
