@@ -126,7 +126,11 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
     const int64_t s = s0 + j + 256 * r;
     const bool ok = s >= 0 && s < T && !(zero_half == 1 && r < 8) && !(zero_half == 2 && r >= 8);
     const int64_t si = reverse ? T - 1 - s : s;
+#ifdef DDSP_FWD_XNT  // A/B: streaming loads of the signal
+    v[r] = make_float2(ok ? __builtin_nontemporal_load(xa + si) : 0.0f, (ok && xb) ? __builtin_nontemporal_load(xb + si) : 0.0f);
+#else
     v[r] = make_float2(ok ? xa[si] : 0.0f, (ok && xb) ? xb[si] : 0.0f);
+#endif
   }
 #ifndef DDSP_PROBE_FWD_NOFFT
   fft4096<false>(v, lds);
@@ -337,8 +341,13 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
     const int64_t s = (int64_t)b * kP + j + 256 * r - kP;
     if (s < T) {
       const int64_t so = reverse ? T - 1 - s : s;
+#ifdef DDSP_INV_YNT  // A/B: streaming stores of the output
+      __builtin_nontemporal_store(v[r].x, ya + so);
+      if (yb) __builtin_nontemporal_store(v[r].y, yb + so);
+#else
       ya[so] = v[r].x;
       if (yb) yb[so] = v[r].y;
+#endif
     }
   }
 }
