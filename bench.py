@@ -672,8 +672,8 @@ def main():
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
         "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region; "
                           "roofline.avg_launch_ms is from inside it.  The synthesis kernel's time depends "
-                          "on what ran before it: after the reverb (the step's order) the chip runs it at "
-                          "~2.2 instead of ~2.38 GHz (in-kernel clock probe, DESIGN.md 3c)",
+                          "on what ran before it (the shader clock it gets after the reverb's MAC, "
+                          "DESIGN.md 3c)",
     }
 
     if syn.reverb is not None and not args.no_uncached_leg:
