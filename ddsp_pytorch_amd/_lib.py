@@ -62,6 +62,7 @@ SIGNATURES = {
     "ddsp_hip_synth_frames": (_I, [_P, _P, _P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64,
                                    _I64, _F, _P]),
     "ddsp_hip_set_persistent_workgroups": (_I, [_I]),
+    "ddsp_hip_set_frame_table": (_I, [_I]),
     "ddsp_hip_synth_frames_controls": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _P, _P, _P, _I64,
                                             _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_synth_frames_counter": (_I, [_P, _P, _P, _F, _U64, _P, _P, _I64, _I64, _I64, _I64, _I64, _F, _P]),

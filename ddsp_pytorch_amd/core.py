@@ -440,6 +440,13 @@ def set_persistent_workgroups(per_cu):
     return int(_lib.query("set_persistent_workgroups", int(per_cu)))
 
 
+def set_frame_table(on):
+    """Launch form of the fused synthesis for launches of many frames (ddsp_hip_set_frame_table):
+    1 = the per-frame controls / filter table first, then the synthesis from it; 0 = one launch;
+    -1 = the default.  Bit-identical results either way.  Returns the previous setting."""
+    return int(_lib.query("set_frame_table", int(on)))
+
+
 def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed, bias=-5.0):
     """synth_frames with on-device noise whose Philox offset is the device word counter[0]
     (int64, advanced by one on the stream after the launch): for calls replayed from a captured

@@ -548,7 +548,60 @@ __device__ __forceinline__ double prep_frame(const float* __restrict__ f0, const
   return S;
 }
 
-template <bool RNG, bool CTRL, bool PAD>
+// The preparation wave's work for one frame when frame_table_kernel has run (TAB): the frame's record
+// (amplitudes, filter taps, S, dinc) into fb, the noise, the filter tail.
+template <bool RNG>
+__device__ __forceinline__ void prep_frame_tab(const float* __restrict__ table, int rec,
+                                               const float* __restrict__ noise, uint32_t k0, uint32_t k1,
+                                               uint32_t off0, uint32_t off1, int H, int bs, int lo_end,
+                                               int tail_start, int pad, int frame, FrameBuf fb, int lane) {
+  const int H4 = (H + 3) & ~3;
+  const float* r = table + (int64_t)frame * rec;
+  const double2 sd = *reinterpret_cast<const double2*>(r);
+  const int ntaps = lo_end + (bs - tail_start);
+  for (int k = lane; k < H4; k += 64) fb.coef()[k] = make_float2((float)(k + 1), r[4 + k]);
+  for (int i = lane; i < ntaps; i += 64) fb.h()[i < lo_end ? i : tail_start + (i - lo_end)] = r[4 + H4 + i];
+  const int quads = bs >> 2;
+  for (int t = lane; t < quads; t += 64) {  // modules.py:119-123
+    float4 v;
+    if (RNG) {
+      const uint64_t q = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
+      const Philox4 p = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
+      v = make_float4(uniform_pm1(p.v[0]), uniform_pm1(p.v[1]), uniform_pm1(p.v[2]), uniform_pm1(p.v[3]));
+    } else {
+      v = *reinterpret_cast<const float4*>(noise + (int64_t)frame * bs + 4 * t);
+    }
+    *reinterpret_cast<float4*>(fb.x() + 4 * t) = v;
+  }
+  for (int i = lane; i < pad; i += 64) fb.x()[i - pad] = 0.0f;
+  wave_lds_sync();  // h, x
+  for (int l = lane; l < bs - tail_start; l += 64) {  // noise tail, in frame_synth's tap order
+    const int j = tail_start + l;
+    const float* hh = fb.h();
+    const float* xx = fb.x();
+    float c = 0.0f;
+    for (int d0 = 0; d0 <= l; d0 += 8) {
+      float hv[8], xv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        hv[q] = hh[j - d0 - q];
+        xv[q] = xx[d0 + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (d0 + q <= l) c = fmaf(hv[q], xv[q], c);
+    }
+    fb.tail()[l] = c;
+  }
+  if (lane == 0) {
+    fb.sc()[0] = sd.x;
+    fb.sc()[1] = sd.y;
+  }
+}
+
+// TAB: frame_table_kernel ran first; `param` is then its table and `ldp` the record's floats (f0, mags,
+// ctrl_out unused: the table kernel wrote the control dicts).
+template <bool RNG, bool CTRL, bool PAD, bool TAB = false>
 __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
@@ -615,9 +668,12 @@ __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
 #ifdef DDSP_PROBE_CLOCK
         if (probe_first < 0) probe_first = fr;
 #endif
-        carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
-                                        bs, sr, lo_end, tail_start, pad, fr, nb, lane, fr == prev + 1, carry_S, ldp,
-                                        ldm);
+        if constexpr (TAB)
+          prep_frame_tab<RNG>(param, ldp, noise, k0, k1, off0, off1, H, bs, lo_end, tail_start, pad, fr, nb, lane);
+        else
+          carry_S = prep_frame<RNG, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, ctrl_out, B, F, H, NB,
+                                          bs, sr, lo_end, tail_start, pad, fr, nb, lane, fr == prev + 1, carry_S, ldp,
+                                          ldm);
       }
       if (lane == 0) *nb.frame() = fr;
       __syncthreads();  // buffer i&1 prepared (or marked empty); the synthesis waves released the other one
@@ -696,6 +752,257 @@ __global__ void __launch_bounds__(320, 5) synth_persist_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-launch form for launches of many frames: the frame table, then the synthesis.
+//
+// Why: a one-workgroup-per-frame launch spends ~22 of a workgroup's ~36 us in the frame's prologue
+// (controls, filter design: dependent global loads, five barriers) — at the start of the launch every
+// resident workgroup is in it with the VALU idle, and the last generation drains at that pace
+// (DESIGN §3c).  frame_table_kernel runs those controls for every frame first (one wave per frame,
+// no workgroup barriers) into a per-frame record in HBM; synth_tab_kernel's prologue is then one load
+// of that record (~0.9 KB), the noise and the tail, and its workgroups are mostly sine loop.
+//
+// Record (floats, 16-B aligned, rec floats per frame): [S (double) | dinc (double) | amplitudes
+// (dist/sum)*amp, H4 | filter taps h[j] for j in [0, lo_end) then [tail_start, bs), ntaps -> 4].
+// Every value is computed by the arithmetic frame_synth uses, and the two fp64 sums in the order of
+// frame_synth's nw-wave thread group (thread 64w + lane: strided partials, a shuffle tree per wave, the
+// waves' totals in order), so the synthesis is bit-identical to synth_frame_kernel's.
+
+// per-wave LDS floats of frame_table_kernel: ct[n4] | A[NB -> 4] | ir[half+1 -> 4] | vals[H4]; with 65 bands
+// the workgroup also holds the 64 x 64 irfft matrix (kTableCosFloats, ahead of the waves' regions)
+constexpr int kTableCosFloats = 64 * 64;
+static __host__ __device__ inline int table_wave_floats(int H, int NB) {
+  const int n = 2 * (NB - 1), half = n >> 1;
+  return ((n + 3) & ~3) + ((NB + 3) & ~3) + ((half + 4) & ~3) + ((H + 3) & ~3);
+}
+
+// One wave per frame.  Latency is the whole cost here (12,800 short chains at config 2), so every global
+// load of a frame is issued up front: the row's f0 values for the prefix, the projections, the
+// magnitudes (registers, first 2 x NT of each; loops past that) and, for 65 bands, the irfft matrix
+// into LDS by the whole workgroup.
+// NW: the waves of frame_synth's thread group (nt / 64 of the launch, 1..4)
+template <bool CTRL, int NW>
+__global__ void __launch_bounds__(512) frame_table_kernel(
+    const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags, float bias,
+    float* __restrict__ ctrl_out, float* __restrict__ table, int B, int F, int H, int NB, int bs, float sr,
+    int lo_end, int tail_start, int rec, int ldp, int ldm) {
+  constexpr int nw = NW;
+  extern __shared__ float4 smem4[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t NF = (int64_t)B * F;
+  const int64_t frame = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;  // one wave per frame
+  const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
+  const int H4 = (H + 3) & ~3;
+  const bool cos_lds = n == 128;
+  float* cosL = reinterpret_cast<float*>(smem4);
+  if (cos_lds) {  // rows k = 0..63 of kIrCos128 (row 0 unused), 8 floats per thread of 512
+    for (int i = threadIdx.x; i < kTableCosFloats / 4; i += blockDim.x)
+      reinterpret_cast<float4*>(cosL)[i] = reinterpret_cast<const float4*>(kIrCos128)[i];
+  }
+  const bool live = frame < NF;
+  const int64_t fr = live ? frame : 0;  // a wave past the last frame only helps with the matrix
+  float* ct = cosL + (cos_lds ? kTableCosFloats : 0) + wv * table_wave_floats(H, NB);
+  float* A = ct + n4;
+  float* ir = A + ((NB + 3) & ~3);
+  float* vals = ir + ((half + 4) & ~3);
+  const int b = (int)(fr / F), f = (int)(fr - (int64_t)b * F);
+  const float* f0b = f0 + (int64_t)b * F;
+  const float* prow = param + fr * ldp;
+  const float* mrow = mags + fr * ldm;
+  const float half_sr = sr * 0.5f;
+  const float pitch0 = f0b[f];
+  const float praw0 = prow[0];
+  const int NT = 64 * nw;
+  // frame_synth's thread t = 64w + lane visits g (and k) = t, t + NT, ...: the first two of each here
+  float fv[NW][2], pv[NW][2], mv[2];
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int g = 64 * w + lane + NT * j;
+      fv[w][j] = g < f ? f0b[g] : 0.0f;
+      pv[w][j] = g < H ? prow[1 + g] : 0.0f;
+    }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) mv[j] = lane + 64 * j < NB ? mrow[lane + 64 * j] : 0.0f;
+  fill_cos_table(ct, n, lane, 64);
+  // the fp64 prefix and dist.sum(-1), summed as frame_synth's group sums them
+  double S = 0.0, D = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    {
+      double ps = 0.0, pd = 0.0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int g = 64 * w + lane + NT * j;
+        if (g < f) ps += (double)bs * (double)phase_inc(fv[w][j], sr);
+        if (g < H) {  // modules.py:53-60 before normalisation
+          const float v = controls_value(pv[w][j], pitch0, g, half_sr);
+          vals[g] = v;
+          pd += (double)v;
+        }
+      }
+      for (int g = 64 * w + lane + 2 * NT; g < f; g += NT) ps += (double)bs * (double)phase_inc(f0b[g], sr);
+      for (int k = 64 * w + lane + 2 * NT; k < H; k += NT) {
+        const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
+        vals[k] = v;
+        pd += (double)v;
+      }
+#ifndef DDSP_PROBE_TAB_NORED
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        ps += __shfl_down(ps, o, 64);
+        pd += __shfl_down(pd, o, 64);
+      }
+      S += __shfl(ps, 0, 64);
+      D += __shfl(pd, 0, 64);
+#else
+      S += ps;
+      D += pd;
+#endif
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    if (lane + 64 * j < NB) A[lane + 64 * j] = scale_fn(mv[j] + bias);  // modules.py:113
+  for (int k = lane + 128; k < NB; k += 64) A[k] = scale_fn(mrow[k] + bias);
+  const float norm = (float)D;
+  const float a = scale_fn(praw0);
+  float* r = table + fr * rec;
+  __syncthreads();  // the matrix; this wave's vals, A, ct
+  if (!live) return;
+  const int64_t BF = NF;
+  for (int k = lane; k < H4; k += 64) {
+    const float v = k < H ? (vals[k] / norm) * a : 0.0f;  // (dist / sum) * amp
+    r[4 + k] = v;
+    if (CTRL && k < H) ctrl_out[BF + frame * H + k] = v;  // modules.py:73's in-place product
+  }
+  if constexpr (CTRL) {
+    if (lane == 0) ctrl_out[frame] = a;
+    for (int k = lane; k < NB; k += 64) ctrl_out[BF * (1 + H) + frame * NB + k] = A[k];
+  }
+  // filter design (core.py:144-166): the irfft's even half, then the rolled/windowed taps
+#ifdef DDSP_PROBE_TAB_NOFILTER
+  if (lane == 0) *reinterpret_cast<double2*>(r) = make_double2(S, (double)phase_inc(pitch0, sr));
+  return;
+#endif
+  if (cos_lds) {
+    const float* cosm = cosL + lane;
+    float s0 = 0.0f, s1 = 0.0f;  // frame_synth's order: s0 odd k, s1 even k, then k = 63 into s0
+#pragma unroll 8
+    for (int k = 1; k < 63; k += 2) {
+      s0 = fmaf(A[k], cosm[k * 64], s0);
+      s1 = fmaf(A[k + 1], cosm[(k + 1) * 64], s1);
+    }
+    s0 = fmaf(A[63], cosm[63 * 64], s0);
+    ir[lane] = (A[0] + ((lane & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
+    float alt = (lane >= 1) ? ((lane & 1) ? -A[lane] : A[lane]) : 0.0f;  // tap n/2: cos(pi k) = (-1)^k
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
+    if (lane == 0) ir[64] = (A[0] + A[64] + 2.0f * alt) * (1.0f / 128.0f);
+  } else {
+    for (int m = lane; m <= half; m += 64) ir[m] = irfft_tap(A, ct, n, m);
+  }
+  wave_lds_sync();  // ir
+  const int ntaps = lo_end + (bs - tail_start);
+  for (int i = lane; i < ntaps; i += 64) {
+    const int j = i < lo_end ? i : tail_start + (i - lo_end);
+    r[4 + H4 + i] = ir_at_half(ir, ct, n, bs, j);
+  }
+  if (lane == 0) *reinterpret_cast<double2*>(r) = make_double2(S, (double)phase_inc(pitch0, sr));
+}
+
+// The synthesis of one frame (f, b) per workgroup from its frame_table_kernel record: noise, filter
+// tail, oscillator bank, FIR, `harmonic + noise` — frame_synth's phases 4-6 with phases 1-3 read back.
+// LDS: coef float2[H4] | h[bs] | tail[half -> 4] | xbuf[pad | bs]
+template <bool RNG, bool PAD>
+__global__ void __launch_bounds__(256) synth_tab_kernel(
+    const float* __restrict__ table, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0,
+    uint32_t off1, const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
+    float* __restrict__ noise_out, int F, int H, int NB, int bs, int lo_end, int tail_start, int pad, int rec) {
+  extern __shared__ float4 smem4[];
+  const int tid = threadIdx.x, NT = blockDim.x;
+  const int half = NB - 1;
+  const int H4 = (H + 3) & ~3;
+  float2* coef = reinterpret_cast<float2*>(smem4);
+  float* h = reinterpret_cast<float*>(coef + H4);
+  float* tail = h + bs;
+  float* xbuf = tail + ((half + 3) & ~3);
+  float* x = xbuf + pad;
+  const int64_t frame = (int64_t)blockIdx.y * F + blockIdx.x;
+  const float* r = table + frame * rec;
+  const double2 sd = *reinterpret_cast<const double2*>(r);  // workgroup-uniform: S, dinc
+  for (int k = tid; k < H4; k += NT) coef[k] = make_float2((float)(k + 1), r[4 + k]);
+  const int ntaps = lo_end + (bs - tail_start);
+  for (int i = tid; i < ntaps; i += NT) h[i < lo_end ? i : tail_start + (i - lo_end)] = r[4 + H4 + i];
+  for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
+  if (RNG && counter) {  // graph-replayed streams: the Philox offset advances in device memory
+    const uint64_t o = (((uint64_t)off1 << 32) | off0) + *counter;
+    off0 = (uint32_t)o;
+    off1 = (uint32_t)(o >> 32);
+  }
+  const int quads = bs >> 2;
+  for (int t = tid; t < quads; t += NT) {  // modules.py:119-123
+    float4 v;
+    if (RNG) {
+      const uint64_t q = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
+      const Philox4 p = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);
+      v = make_float4(uniform_pm1(p.v[0]), uniform_pm1(p.v[1]), uniform_pm1(p.v[2]), uniform_pm1(p.v[3]));
+    } else {
+      v = *reinterpret_cast<const float4*>(noise + frame * bs + 4 * t);
+    }
+    *reinterpret_cast<float4*>(x + 4 * t) = v;
+  }
+  __syncthreads();
+  // noise tail (taps past bs - n/2 reach only the last n/2 outputs)
+  for (int l = tid; l < bs - tail_start; l += NT) {
+    const int j = tail_start + l;
+    float c = 0.0f;
+    for (int d = 0; d <= l; ++d) c = fmaf(h[j - d], x[d], c);
+    tail[l] = c;
+  }
+  // oscillator bank for samples [j0, j0+4)
+  const int j0 = 4 * tid;
+  const bool active = j0 < bs;
+  float w[4], acc[4];
+  bool fast = true;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w[s] = (float)(sd.x + (double)(j0 + s + 1) * sd.y);  // omega = fl32(exact prefix)
+    acc[s] = 0.0f;
+    fast = fast && (fabsf(w[s]) * (float)H4 < kFastArgLimit);
+  }
+  // loop placement as in frame_synth (tools/loop_align.py; tests/test_loop_align.py pins it)
+  if constexpr (PAD) asm volatile(".p2align 3\n s_nop 0");
+  else asm volatile(".p2align 3");
+  if (active) {
+    if (fast) {
+      osc_bank4(coef, H4, w, acc);
+    } else {
+      for (int k = 0; k < H; ++k) {
+        const float2 c = coef[k];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float xx = w[s] * c.x;
+          acc[s] = fmaf(fabsf(xx) < kFastArgLimit ? sin_reduced(xx) : sin_slow(xx), c.y, acc[s]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // tail[] complete
+  if (!active) return;
+  const float4 y = fir4(h, x, j0, lo_end, bs, bs);  // taps [0, lo_end); the wrapped taps are in tail[]
+  float nz[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if (j0 + s >= tail_start) nz[s] += tail[j0 + s - tail_start];
+  const int64_t o = frame * bs + j0;
+  if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (noise_out) *reinterpret_cast<float4*>(noise_out + o) = make_float4(nz[0], nz[1], nz[2], nz[3]);
+  *reinterpret_cast<float4*>(out + o) =
+      make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121
+}
+
 __global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
 
 }  // namespace
@@ -710,6 +1017,14 @@ constexpr bool kSynthForwardPad = false;
 // sine-loop placement padding of the persistent instantiations (tools/loop_align.py)
 template <bool RNG, bool CTRL>
 constexpr bool kPersistPad = false;
+
+// sine-loop placement padding of the frame-table synthesis instantiations (tools/loop_align.py)
+template <bool RNG>
+constexpr bool kTabPad = true;
+
+// sine-loop placement padding of the persistent instantiations fed by the frame table
+template <bool RNG>
+constexpr bool kPersistTabPad = false;
 
 
 namespace ddsp {
@@ -880,6 +1195,42 @@ static size_t persist_lds_floor(int wpc) {
   return pad && wpc > 0 ? (size_t)(160 * 1024 / (wpc + 1) + 1024) : 0;
 }
 
+// the two-launch form (frame_table_kernel + synth_tab_kernel) for launches of many frames:
+// ddsp_hip_set_frame_table, else DDSP_HIP_FRAME_TABLE, else off (measured slower in the bench step: the
+// synthesis launch gains ~20 us, the table launch costs ~26 us)
+static std::atomic<int> g_frame_table{-1};
+static int frame_table_on() {
+  const int v = g_frame_table.load(std::memory_order_relaxed);
+  if (v >= 0) return v;
+  const char* e = getenv("DDSP_HIP_FRAME_TABLE");
+  return e ? atoi(e) != 0 : 0;
+}
+
+// frame_table_kernel's records: one grow-only device buffer per (device, stream), so launches on one
+// stream (ordered) reuse it.  Never taken while the stream is capturing a graph (nullptr: the caller
+// runs the one-launch kernel), so no graph holds one; a smaller buffer left by growth stays allocated.
+static float* frame_table_buffer(void* stream, size_t floats) {
+  static std::mutex mu;
+  static std::map<std::pair<int, void*>, std::pair<float*, size_t>> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(S(stream), &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  auto& slot = slots[{dev, stream}];
+  if (slot.second >= floats) return slot.first;
+  float* p = nullptr;
+  if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  slot = {p, floats};
+  return p;
+}
+
 // a frame's LDS layout (frame_synth): the FIR's first run [0, lo_end) and the wrapped taps from
 // tail_start, the zero padding ahead of the samples, and the floats of one frame buffer
 struct FrameShape {
@@ -936,8 +1287,38 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   const size_t shm = sizeof(float) * (floats + (G > 1 ? (size_t)bs : 0));
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
-  // many frames: the persistent, wave-specialised kernel (frame ranges per workgroup)
   const int64_t NF = batch * frames;
+  // many frames: the frames' controls, filter taps and phase prefixes into a table first (one wave per
+  // frame), then a synthesis kernel reading it
+  float* table = nullptr;
+  const int H4 = ((int)n_harmonic + 3) & ~3;
+  const int ntaps = lo_end + (bs - tail_start);
+  const int rec = 4 + H4 + ((ntaps + 3) & ~3);
+  const int twf = table_wave_floats((int)n_harmonic, (int)n_bands);
+  const int tcos = n_bands == 65 ? kTableCosFloats : 0;
+  // frames (waves) per workgroup: 8, fewer when their LDS would not fit (the matrix is read once per workgroup)
+  const int tpg = (int)std::max<int64_t>(1, std::min<int64_t>(8, (48 * 1024) / (sizeof(float) * (size_t)twf)));
+  if (G == 1 && NF <= INT32_MAX && frame_table_on() && ((size_t)tpg * twf + tcos) * sizeof(float) <= 64 * 1024 &&
+      (table = frame_table_buffer(stream, (size_t)NF * rec)) != nullptr) {
+    const unsigned tgrid = (unsigned)((NF + tpg - 1) / tpg);
+    const size_t tshm = sizeof(float) * ((size_t)tpg * twf + tcos);
+#define DDSP_TABLE_LAUNCH(CTRL_, NW_)                                                                      \
+    hipLaunchKernelGGL((frame_table_kernel<CTRL_, NW_>), dim3(tgrid), dim3(64 * tpg), tshm, S(stream), f0, param, \
+                       raw_magnitudes, bias, controls_out, table, (int)batch, (int)frames, (int)n_harmonic,       \
+                       (int)n_bands, bs, sample_rate, lo_end, tail_start, rec, (int)param_ld, (int)mags_ld)
+#define DDSP_TABLE_LAUNCH_NW(CTRL_)                \
+    switch (nt / 64) {                             \
+      case 1: DDSP_TABLE_LAUNCH(CTRL_, 1); break;  \
+      case 2: DDSP_TABLE_LAUNCH(CTRL_, 2); break;  \
+      case 3: DDSP_TABLE_LAUNCH(CTRL_, 3); break;  \
+      default: DDSP_TABLE_LAUNCH(CTRL_, 4); break; \
+    }
+    if (controls_out) DDSP_TABLE_LAUNCH_NW(true)
+    else DDSP_TABLE_LAUNCH_NW(false)
+#undef DDSP_TABLE_LAUNCH_NW
+#undef DDSP_TABLE_LAUNCH
+  }
+  // many frames: the persistent, wave-specialised kernel (frame ranges per workgroup)
   const int cus = device_cus();
   const int wpc = persist_wgs_per_cu();
   const int buf_floats = (int)((floats + 8 + 3) & ~(size_t)3);
@@ -954,7 +1335,16 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
                        RNG_ ? counter : nullptr, out, harmonic_out, noise_out, controls_out, (int)batch,          \
                        (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats, \
                        tickets, (int)param_ld, (int)mags_ld)
-    if (noise) {
+#define DDSP_SYNTH_PERSIST_TAB_LAUNCH(RNG_)                                                                \
+    hipLaunchKernelGGL((synth_persist_kernel<RNG_, false, kPersistTabPad<RNG_>, true>), dim3(pgrid), pblock, lds, \
+                       S(stream), f0, table, raw_magnitudes, bias, RNG_ ? nullptr : noise, k0, k1, o0, o1,        \
+                       RNG_ ? counter : nullptr, out, harmonic_out, noise_out, nullptr, (int)batch,               \
+                       (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, tail_start, pad, buf_floats, \
+                       tickets, rec, (int)mags_ld)
+    if (table) {
+      if (noise) DDSP_SYNTH_PERSIST_TAB_LAUNCH(false);
+      else DDSP_SYNTH_PERSIST_TAB_LAUNCH(true);
+    } else if (noise) {
       if (controls_out) DDSP_SYNTH_PERSIST_LAUNCH(false, true);
       else DDSP_SYNTH_PERSIST_LAUNCH(false, false);
     } else {
@@ -962,11 +1352,26 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
       else DDSP_SYNTH_PERSIST_LAUNCH(true, false);
     }
 #undef DDSP_SYNTH_PERSIST_LAUNCH
+#undef DDSP_SYNTH_PERSIST_TAB_LAUNCH
     if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
     return launch_status();
   }
   const dim3 grid((unsigned)frames, (unsigned)batch), block((unsigned)(nt * G));
-#define DDSP_SYNTH_FRAME_LAUNCH(RNG_, SPLIT_)                                                              \
+  if (table) {
+    const int half = (int)n_bands - 1;
+    const size_t sshm = sizeof(float) * ((size_t)2 * H4 + bs + ((half + 3) & ~3) + pad + bs);
+    if (noise)
+      hipLaunchKernelGGL((synth_tab_kernel<false, kTabPad<false>>), grid, dim3(nt), sshm, S(stream), table, noise, k0,
+                         k1, o0, o1, nullptr, out, harmonic_out, noise_out, (int)frames, (int)n_harmonic,
+                         (int)n_bands, bs, lo_end, tail_start, pad, rec);
+    else
+      hipLaunchKernelGGL((synth_tab_kernel<true, kTabPad<true>>), grid, dim3(nt), sshm, S(stream), table, nullptr, k0,
+                         k1, o0, o1, counter, out, harmonic_out, noise_out, (int)frames, (int)n_harmonic,
+                         (int)n_bands, bs, lo_end, tail_start, pad, rec);
+    if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
+    return launch_status();
+  }
+#define DDSP_SYNTH_FRAME_LAUNCH(RNG_, SPLIT_)                                                             \
   do {                                                                                                  \
     if (controls_out) DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, true);                                       \
     else DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, false);                                                  \
@@ -991,6 +1396,10 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
 
 int ddsp_hip_set_persistent_workgroups(int per_cu) {
   return g_persist_wpc.exchange(per_cu < 0 ? -1 : per_cu);
+}
+
+int ddsp_hip_set_frame_table(int on) {
+  return g_frame_table.exchange(on < 0 ? -1 : (on != 0));
 }
 
 int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_magnitudes, float bias,

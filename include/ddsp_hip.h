@@ -147,6 +147,15 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
  * any thread, applies to later launches); returns the previous setting. */
 int ddsp_hip_set_persistent_workgroups(int per_cu);
 
+/* Launch form of ddsp_hip_synth_frames* for many frames (the one-workgroup-per-frame shape): 1 = two
+ * launches, the frames' controls, filter design and phase prefixes into a per-frame table first (one
+ * wave per frame; a library-owned device buffer per stream), then the synthesis reading it; 0 = one
+ * launch doing both per frame; -1 restores the default (DDSP_HIP_FRAME_TABLE, else 0: the two launches
+ * measured slower).  Results are
+ * bit-identical either way.  Launches on a stream that is capturing a graph always take one launch.
+ * Process-wide (an atomic); returns the previous setting. */
+int ddsp_hip_set_frame_table(int on);
+
 /* ddsp_hip_synth_frames that also writes the controls DDSPDecoder.forward returns
  * (decoder.py:127-135: output['harmonic_ctrls'], output['noise_ctrls']) into controls_out (nullable),
  * laid out as [amplitudes B*F | harmonic_distribution B*F*H | magnitudes B*F*NB]: amplitudes =
