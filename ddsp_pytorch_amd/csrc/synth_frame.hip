@@ -793,7 +793,11 @@ __global__ void __launch_bounds__(512) frame_table_kernel(
   const int64_t frame = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;  // one wave per frame
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
+#ifdef DDSP_PROBE_TAB_NOMAT
+  const bool cos_lds = false;
+#else
   const bool cos_lds = n == 128;
+#endif
   float* cosL = reinterpret_cast<float*>(smem4);
   if (cos_lds) {  // rows k = 0..63 of kIrCos128 (row 0 unused), 8 floats per thread of 512
     for (int i = threadIdx.x; i < kTableCosFloats / 4; i += blockDim.x)
@@ -837,7 +841,11 @@ __global__ void __launch_bounds__(512) frame_table_kernel(
         const int g = 64 * w + lane + NT * j;
         if (g < f) ps += (double)bs * (double)phase_inc(fv[w][j], sr);
         if (g < H) {  // modules.py:53-60 before normalisation
+#ifdef DDSP_PROBE_TAB_NOCTRL
+          const float v = pv[w][j];
+#else
           const float v = controls_value(pv[w][j], pitch0, g, half_sr);
+#endif
           vals[g] = v;
           pd += (double)v;
         }
@@ -869,7 +877,11 @@ __global__ void __launch_bounds__(512) frame_table_kernel(
   const float norm = (float)D;
   const float a = scale_fn(praw0);
   float* r = table + fr * rec;
+#ifdef DDSP_PROBE_TAB_NOMAT
+  wave_lds_sync();
+#else
   __syncthreads();  // the matrix; this wave's vals, A, ct
+#endif
   if (!live) return;
   const int64_t BF = NF;
   for (int k = lane; k < H4; k += 64) {
