@@ -805,6 +805,10 @@ __global__ void __launch_bounds__(512) frame_table_kernel(
   }
   const bool live = frame < NF;
   const int64_t fr = live ? frame : 0;  // a wave past the last frame only helps with the matrix
+#ifdef DDSP_PROBE_TAB_EMPTY  // launch-shape floor: one store per frame
+  if (live && lane == 0) table[fr * rec] = 0.0f;
+  return;
+#endif
   float* ct = cosL + (cos_lds ? kTableCosFloats : 0) + wv * table_wave_floats(H, NB);
   float* A = ct + n4;
   float* ir = A + ((NB + 3) & ~3);
@@ -829,6 +833,20 @@ __global__ void __launch_bounds__(512) frame_table_kernel(
     }
 #pragma unroll
   for (int j = 0; j < 2; ++j) mv[j] = lane + 64 * j < NB ? mrow[lane + 64 * j] : 0.0f;
+#ifdef DDSP_PROBE_TAB_LOADS  // loads of the frame and its record's stores, no arithmetic
+  if (live) {
+    float* rr = table + fr * rec;
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int g = 64 * w + lane + NT * j;
+        if (g < H4) rr[4 + g] = pv[w][j] + fv[w][j];
+      }
+    if (lane < rec - 4 - H4) rr[4 + H4 + lane] = mv[0] + mv[1] + pitch0 + praw0;
+  }
+  return;
+#endif
   fill_cos_table(ct, n, lane, 64);
   // the fp64 prefix and dist.sum(-1), summed as frame_synth's group sums them
   double S = 0.0, D = 0.0;
