@@ -82,12 +82,24 @@ __device__ __forceinline__ bool frame_synth(
   if (false)
 #endif
   for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
-  for (int k = tid; k < H; k += NT) {  // modules.py:53-60 before normalisation
-    const float v = controls_value(prow[1 + k], pitch0, k, half_sr);
-    coef[k].y = v;
-    part_d += (double)v;
+  // the frame's H + NB + 1 scale_function values as one work list (item i at thread i mod NT, in
+  // ascending i, so the distribution's partial sums keep their order): harmonic distribution
+  // (modules.py:53-60 before normalisation), noise magnitudes (modules.py:113), then the amplitude
+  // (modules.py:52), published through tail[0], which phase 4 overwrites only after it is read
+  for (int i = tid; i < H + NB + 1; i += NT) {
+    const float* src = i < H ? prow + 1 + i : (i < H + NB ? mags + frame * ldm + (i - H) : prow);
+    const float raw = *src;
+    const float sv = scale_fn(i >= H && i < H + NB ? raw + bias : raw);
+    if (i < H) {
+      const float v = sv * ((pitch0 * (float)(i + 1)) < half_sr ? kOnePlusEps : kEps);  // controls_value
+      coef[i].y = v;
+      part_d += (double)v;
+    } else if (i < H + NB) {
+      A[i - H] = sv;
+    } else {
+      tail[0] = sv;
+    }
   }
-  for (int k = tid; k < NB; k += NT) A[k] = scale_fn(mags[frame * ldm + k] + bias);  // modules.py:113
   fill_cos_table(ct, n, tid, NT);
   for (int i = tid; i < pad; i += NT) xbuf[i] = 0.0f;
   const int quads = bs >> 2;
@@ -110,7 +122,7 @@ __device__ __forceinline__ bool frame_synth(
   group_sum_double2(part_s, part_d, red, w0, NT >> 6);  // includes the barrier that publishes phase 1
   const double S = part_s;                 // exact fp64 prefix over earlier frames
   const float norm = (float)part_d;        // dist.sum(-1)
-  const float a = scale_fn(prow[0]);
+  const float a = tail[0];                 // scale_function(amplitude)
 
   // ---- phase 2: harmonic coefficient table; even half of the noise filter taps ----
   for (int k = tid; k < H4; k += NT) {
@@ -244,7 +256,7 @@ __device__ __forceinline__ bool frame_synth(
     float* co = ctrl_out;
     asm volatile("" : "+s"(co));
     const int64_t BF = (int64_t)B * F;
-    if (tid == 0) co[frame] = scale_fn(prow[0]);
+    if (tid == 0) co[frame] = a;
     for (int k = tid; k < H; k += NT) co[BF + frame * H + k] = coef[k].y;
     for (int k = tid; k < NB; k += NT) co[BF * (1 + H) + frame * NB + k] = A[k];
   }
