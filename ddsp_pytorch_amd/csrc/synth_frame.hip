@@ -158,12 +158,25 @@ __device__ __forceinline__ bool frame_synth(
     const int j = i < nlo ? i : tail_start + (i - nlo);
     h[j] = ir_at_half(ir, ct, n, bs, j);
   }
+  if (bs - tail_start == 64 && bs - 127 >= lo_end && tid < 63) h[tail_start - 63 + tid] = 0.0f;  // phase 4's padding
   __syncthreads();
 
   // ---- phase 4: noise tail (taps past bs - n/2 reach only the last n/2 outputs) ----
 #ifdef DDSP_PROBE_NO_TAIL
   if (false)
 #endif
+  // with n/2 = 64 (65 bands) and h zero for the 63 positions below tail_start (written in phase 3) every
+  // lane runs the same 64 taps, unrolled with no per-tap predication: the taps past l add fma(0, x, c) = c,
+  // the others come in tap order, so the sums are the loop's below (measured 1.2 % faster)
+  if (bs - tail_start == 64 && bs - 127 >= lo_end) {
+    for (int l = tid; l < 64; l += NT) {
+      const float* hj = h + tail_start + l;
+      float c = 0.0f;
+#pragma unroll 16
+      for (int d = 0; d < 64; ++d) c = fmaf(hj[-d], x[d], c);
+      tail[l] = c;
+    }
+  } else
   for (int l = tid; l < bs - tail_start; l += NT) {
     const int j = tail_start + l;
     float c = 0.0f;
