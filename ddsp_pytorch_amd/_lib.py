@@ -61,19 +61,11 @@ SIGNATURES = {
     "ddsp_hip_filtered_noise_params": (_I, [_P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "ddsp_hip_synth_frames": (_I, [_P, _P, _P, _F, _P, _U64, _U64, _P, _P, _P, _I64, _I64, _I64, _I64,
                                    _I64, _F, _P]),
-    "ddsp_hip_set_persistent_workgroups": (_I, [_I]),
-    "ddsp_hip_set_frame_table": (_I, [_I]),
     "ddsp_hip_synth_frames_controls": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _P, _P, _P, _I64,
                                             _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_synth_frames_counter": (_I, [_P, _P, _P, _F, _U64, _P, _P, _I64, _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_reverb_build_impulse": (_I, [_P, _P, _P, _P, _I64, _F, _P]),
     "ddsp_hip_reverb_spectrum_floats": (_SZ, [_I64, _I64]),
-    "ddsp_hip_synth_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
-    "ddsp_hip_synth_reverb_spectra": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _SZ, _I64, _I64, _I64,
-                                           _I64, _I64, _F, _P]),
-    "ddsp_hip_reverb_apply_spectra": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
-    "ddsp_hip_synth_reverb": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _I64, _P, _P, _SZ, _I64, _I64,
-                                   _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_reverb_workspace_size": (_SZ, [_I64, _I64, _I64]),
     "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P]),
     "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),

@@ -433,20 +433,6 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     return (*res, cd) if parts else (res, cd)
 
 
-def set_persistent_workgroups(per_cu):
-    """Launch shape of the fused synthesis kernel for launches of many frames
-    (ddsp_hip_set_persistent_workgroups): persistent workgroups per CU, 0 = one workgroup per frame,
-    -1 = the default.  Returns the previous setting."""
-    return int(_lib.query("set_persistent_workgroups", int(per_cu)))
-
-
-def set_frame_table(on):
-    """Launch form of the fused synthesis for launches of many frames (ddsp_hip_set_frame_table):
-    1 = the per-frame controls / filter table first, then the synthesis from it; 0 = one launch;
-    -1 = the default.  Bit-identical results either way.  Returns the previous setting."""
-    return int(_lib.query("set_frame_table", int(on)))
-
-
 def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed, bias=-5.0):
     """synth_frames with on-device noise whose Philox offset is the device word counter[0]
     (int64, advanced by one on the stream after the launch): for calls replayed from a captured
@@ -466,74 +452,6 @@ def synth_frames_counter(f0, param, mags, block_size, sample_rate, counter, seed
     _lib.call("synth_frames_counter", _lib.ptr(_c(f0)), _lib.ptr(_c(param)), _lib.ptr(_c(mags)), float(bias),
               int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(counter), _lib.ptr(out), B, F, H1 - 1, NB, bs,
               float(sample_rate), _lib.stream_of(out))
-    return out
-
-
-def synth_reverb(f0, param, mags, block_size, sample_rate, spectrum, ir_length, bias=-5.0, noise=None):
-    """decoder.py:106-125's synthesis section followed by Reverb.forward (modules.py:28-35):
-    reverb(harmonic + noise) [B, F*bs, 1] from the raw projections, with ``spectrum`` the reverb's
-    cached IR spectrum for n_samples = F*bs (``reverb_spectrum``; ``Reverb._spectrum``).
-
-    One synthesis launch writes the reverb's input-block spectra directly (``synth_reverb_spectra``:
-    the dry signal never goes to HBM), then the partitioned convolution's multiply-accumulate and
-    inverse kernels (``reverb_apply_spectra``).  Outside that kernel's envelope (block_size dividing
-    2048, 256..1024) or under autograd, the same result comes from ``synth_frames`` then
-    ``reverb_apply``.  Noise as in ``synth_frames`` (device Philox: one offset per call)."""
-    z = synth_reverb_spectra(f0, param, mags, block_size, sample_rate, bias=bias, noise=noise)
-    if isinstance(z, torch.Tensor):
-        return reverb_apply_spectra(z, spectrum, ir_length, f0.shape[0], f0.shape[1] * int(block_size))
-    if z is None:
-        return None
-    return reverb_apply(z[1], spectrum, ir_length)
-
-
-def synth_reverb_spectra(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None):
-    """The first half of ``synth_reverb``: the fused synthesis launch writing the partitioned
-    convolution's input spectra (``ddsp_hip_synth_reverb_spectra``; [pairs, blocks, 4096] complex)
-    -> that tensor.  Outside its envelope or under autograd -> ("signal", dry signal) from
-    ``synth_frames`` (None when that is outside the fused envelope as well)."""
-    _dev(f0, param, mags)
-    B, F, H1 = param.shape
-    NB = mags.shape[-1]
-    bs = int(block_size)
-    if f0.shape != (B, F, 1) or mags.shape[:2] != (B, F) or H1 < 2:
-        raise RuntimeError("synth_reverb: f0 [B,F,1], param [B,F,H+1], mags [B,F,NB] expected")
-    if _wants_grad(f0, param, mags) or not synth_frames_in_envelope(H1 - 1, NB, bs, B):
-        sig = synth_frames(f0, param, mags, bs, sample_rate, bias=bias, noise=noise)
-        return None if sig is None else ("signal", sig)
-    if noise is not None:
-        _dev(noise)
-        if tuple(noise.shape) != (B, F, bs):
-            raise RuntimeError(f"synth_reverb: noise must be [B, F, block_size] = {(B, F, bs)}")
-        noise = _c(noise)
-    f0c = _c(f0)
-    (pc, ldp), (mc, ldm) = _frame_rows(param), _frame_rows(mags)
-    T = F * bs
-    nbytes = int(_lib.query("reverb_input_spectra_bytes", B, T))
-    z = torch.empty(nbytes // 4, dtype=torch.float32, device=f0.device)
-    seed, offset = _noise_counter.next() if noise is None else (0, 0)
-    st = _lib.call("synth_reverb_spectra", _lib.ptr(f0c), _lib.ptr(pc), ldp, _lib.ptr(mc), ldm, float(bias),
-                   _lib.ptr(noise), seed, offset, _lib.ptr(z), nbytes, B, F, H1 - 1, NB, bs, float(sample_rate),
-                   _lib.stream_of(z), allow=(ERANGE,))
-    if st == ERANGE:  # outside the fused transform's envelope: the same noise draw, two launch groups
-        return ("signal", _synth_frames_launch(f0, param, mags, bs, sample_rate, bias, noise, False, seed, offset))
-    return z
-
-
-def reverb_apply_spectra(spectra, spectrum, ir_length, batch, n_samples):
-    """Reverb.forward (modules.py:28-35) from the input spectra ``synth_reverb_spectra`` wrote:
-    the partitioned convolution's multiply-accumulate and inverse kernels -> [B, T, 1]."""
-    _dev(spectra, spectrum)
-    B, T = int(batch), int(n_samples)
-    if spectrum.numel() != reverb_spectrum_floats(T, ir_length):
-        raise RuntimeError("reverb_apply_spectra: spectrum was computed for a different length")
-    nbytes = int(_lib.query("reverb_input_spectra_bytes", B, T))
-    if spectra.numel() * spectra.element_size() < nbytes:
-        raise RuntimeError("reverb_apply_spectra: input spectra too small for (batch, n_samples)")
-    out = torch.empty(B, T, 1, dtype=torch.float32, device=spectra.device)
-    ws = _workspace(nbytes, spectra.device)
-    _lib.call("reverb_apply_spectra", _lib.ptr(spectra), _lib.ptr(spectrum), _lib.ptr(out), B, T, int(ir_length),
-              _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
     return out
 
 

@@ -532,14 +532,8 @@ unsigned grid1d(int64_t n, int per_block) {
 
 // Harmonic backward geometry: NS sample segments so that ceil(H/4) x NS fills about
 // kBwdThreads threads (small workgroups: several per CU hide each one's latency-bound phases).
-int bwd_threads() {
-  static int v = [] {
-    const char* e = getenv("DDSP_HIP_BWD_THREADS");  // tuning knob (64..512)
-    const int t = e ? atoi(e) : 128;  // measured best at config 2 (64..512 swept)
-    return std::max(64, std::min(512, (t / 64) * 64));
-  }();
-  return v;
-}
+constexpr int kBwdThreads = 128;  // measured best at config 2 (64..512 swept)
+int bwd_threads() { return kBwdThreads; }
 
 void harmonic_backward_shape(int H, int bs, int& nt, int& ns) {
   const int kq = (H + kKPT - 1) / kKPT;
@@ -671,14 +665,7 @@ int ddsp_hip_synth_frames_backward(const float* f0, const float* param, const fl
     return DDSP_HIP_EINVAL;
   // The two halves as two launches on the stream: measured faster than the one-launch form whose
   // extra wave ran the noise VJP beside the sine waves (config 2, tools/exp_bwd_split.py: 176.7 vs
-  // 187.6-190.3 us; the halves alone 130.4 and 47.9 us, on two streams 223 us).  That form stays
-  // reachable as DDSP_BWD_FUSED for A/B.
-#ifdef DDSP_BWD_FUSED
-  if (!grad_noise || grad_noise == grad_harmonic)
-    return frame_backward_launch(2, noise ? 1 : 2, true, f0, grad_harmonic, param, nullptr, nullptr, grad_param,
-                                 nullptr, nullptr, batch, frames, n_harmonic, block_size, sample_rate,
-                                 raw_magnitudes, noise, seed, offset, bias, grad_magnitudes, n_bands, stream);
-#endif
+  // 187.6-190.3 us; the halves alone 130.4 and 47.9 us, on two streams 223 us).
   int st = frame_backward_launch(2, 0, false, f0, grad_harmonic, param, nullptr, nullptr, grad_param, nullptr,
                                  nullptr, batch, frames, n_harmonic, block_size, sample_rate, nullptr, nullptr, 0,
                                  0, 0.0f, nullptr, 0, stream);

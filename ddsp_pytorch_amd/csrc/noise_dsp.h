@@ -89,9 +89,6 @@ static __device__ __forceinline__ float4 fir4(const float* __restrict__ h, const
   float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
   auto run = [&](int m_begin, int m_end) {
     float4 cur = x4[q0 - (m_begin >> 2)];  // x[j0-m .. j0-m+3]
-#ifdef DDSP_FIR_UNROLL2
-#pragma unroll 2
-#endif
     for (int m4 = m_begin >> 2; m4 < (m_end >> 2); ++m4) {
       const float4 prv = x4[q0 - m4 - 1];  // x[j0-m-4 .. j0-m-1]
       const float4 hh = h4[m4];

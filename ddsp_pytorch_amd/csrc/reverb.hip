@@ -149,17 +149,6 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                      workspace, workspace_bytes, stream);
 }
 
-int ddsp_hip_reverb_apply_spectra(const float* input_spectra, const float* spectrum, float* out, int64_t batch,
-                                  int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
-                                  void* stream) {
-  if (batch < 0 || n_samples < 1 || ir_length < 1) return DDSP_HIP_EINVAL;
-  if (batch == 0) return DDSP_HIP_OK;
-  if (!input_spectra || !spectrum || !out) return DDSP_HIP_EINVAL;
-  if (!workspace || workspace_bytes < upols_spectra_bytes(batch, n_samples)) return DDSP_HIP_EWORKSPACE;
-  return upols_apply_spectra(reinterpret_cast<const float2*>(input_spectra), batch, n_samples, spectrum,
-                             std::min(ir_length, n_samples), false, out, reinterpret_cast<float2*>(workspace), stream);
-}
-
 int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, float* grad_x, int64_t batch,
                                      int64_t n_samples, int64_t ir_length, void* workspace,
                                      size_t workspace_bytes, void* stream) {

@@ -71,27 +71,12 @@ __device__ __forceinline__ void cmac(v2f& acc, float2 a, v2f b, v2f b_rot) {
   acc = __builtin_elementwise_fma((v2f){a.y, a.y}, b_rot, acc);
 }
 
-// MAC variants, compile-time (tools/ab_build.sh -D...): the shipped MAC is the register-ring kernel
-// (UPOLS_MAC_RING=1, 25 blocks, prefetch 3, G ring 3); UPOLS_MAC_RING=0 builds the shifting-window
-// kernel it replaced (29.3 vs 25.7-26.7 us at config 2), kept as the A/B baseline
-#ifndef UPOLS_MAC_BLK
-#define UPOLS_MAC_BLK 25
-#endif
-#ifndef UPOLS_MAC_RING
-#define UPOLS_MAC_RING 1
-#endif
-#ifndef UPOLS_RING_BLK
-#define UPOLS_RING_BLK 25
-#endif
-#ifndef UPOLS_RING_PF
-#define UPOLS_RING_PF 3
-#endif
-#ifndef UPOLS_RING_GR
-#define UPOLS_RING_GR 3
-#endif
-#ifndef UPOLS_RING_WAVES
-#define UPOLS_RING_WAVES 1
-#endif
+// MAC shape: the register-ring kernel, 25 output blocks per thread, operands prefetched 3 steps
+// ahead, a G ring of 3 (25.7-26.7 us at config 2 against 29.3 us for the shifting
+// window it replaced)
+constexpr int kRingBlk = 25;
+constexpr int kRingPF = 3;
+constexpr int kRingGR = 3;
 
 // rows of the packed signal: pair -> (row_a, row_b or -1)
 __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& ra, int& rb) {
@@ -126,28 +111,12 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
     const int64_t s = s0 + j + 256 * r;
     const bool ok = s >= 0 && s < T && !(zero_half == 1 && r < 8) && !(zero_half == 2 && r >= 8);
     const int64_t si = reverse ? T - 1 - s : s;
-#ifdef DDSP_FWD_XNT  // A/B: streaming loads of the signal
-    v[r] = make_float2(ok ? __builtin_nontemporal_load(xa + si) : 0.0f, (ok && xb) ? __builtin_nontemporal_load(xb + si) : 0.0f);
-#else
     v[r] = make_float2(ok ? xa[si] : 0.0f, (ok && xb) ? xb[si] : 0.0f);
-#endif
   }
-#ifndef DDSP_PROBE_FWD_NOFFT
   fft4096<false>(v, lds);
-#endif
   float2* out = X + ((int64_t)pair * nb + b) * kN;
-#ifdef DDSP_PROBE_FWD_NOSTORE
-  if (v[3].x == 1234.5f)
-#endif
-#ifdef DDSP_FWD_NT  // A/B: streaming (non-temporal) stores of the spectra
-  typedef float f2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    __builtin_nontemporal_store((f2v){v[r].x, v[r].y}, reinterpret_cast<f2v*>(out + j + 256 * r));
-#else
 #pragma unroll
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
-#endif
 }
 
 // 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
@@ -184,58 +153,6 @@ __global__ void __launch_bounds__(kNT) upols_kernel_spectrum_kernel(const float*
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
 }
 
-// Y[pair][b][f] = sum_q Z[pair][b-q][f] * G[q][f] (Q here = the number of kernel spectra, Q+1 of
-// the header); each thread one bin, BLK consecutive blocks
-// with a sliding window of X in registers.  grid (N/256, ceil(nb/BLK), npairs)
-// (Measured: a register double-buffered prefetch of the next partitions ran 5-10% slower — the
-// extra registers cost more occupancy than the hidden latency bought.)
-template <int BLK>
-__global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict__ X,
-                                                        const float2* __restrict__ Hs,
-                                                        int64_t h_pair_stride, int nb, int Q,
-                                                        float2* __restrict__ Y) {
-  const int f = blockIdx.x * kNT + threadIdx.x;
-  // chunks end-aligned: the partial chunk is the first one, whose blocks see the fewest
-  // partitions (min(Q, b0 + BLK) iterations), instead of a nearly empty last chunk paying Q
-  const int b0 = nb - (int)(gridDim.y - blockIdx.y) * BLK;
-  const int pair = blockIdx.z;
-  const float2* Xp = X + (int64_t)pair * nb * kN + f;
-  const float2* Hp = Hs + (int64_t)pair * h_pair_stride + f;
-  const float2 zero = make_float2(0.f, 0.f);
-  float2 win[BLK];
-  v2f acc[BLK];
-#pragma unroll
-  for (int d = 0; d < BLK; ++d) {
-    acc[d] = (v2f){0.f, 0.f};
-    // clamped load + value select (a select of pointers made hipcc go through scratch)
-    const float2 xv = Xp[(int64_t)max(b0 + d, 0) * kN];
-    win[d] = b0 + d >= 0 ? xv : zero;
-  }
-  const int pmax = min(Q, b0 + BLK);
-#pragma unroll 4
-  for (int p = 0; p < pmax; ++p) {
-    const float2 h = Hp[(int64_t)p * kN];
-    const v2f hb = {h.x, h.y}, hr = {-h.y, h.x};
-#pragma unroll
-    for (int d = 0; d < BLK; ++d) cmac(acc[d], win[d], hb, hr);
-#pragma unroll
-    for (int d = BLK - 1; d > 0; --d) win[d] = win[d - 1];
-    const int bn = b0 - p - 1;
-    const float2 xv = Xp[(int64_t)max(bn, 0) * kN];
-    win[0] = bn >= 0 ? xv : zero;
-  }
-  float2* Yp = Y + (int64_t)pair * nb * kN + f;
-#ifdef DDSP_MAC_YNT  // A/B: streaming stores of Y
-#pragma unroll
-  for (int d = 0; d < BLK; ++d)
-    if (b0 + d >= 0) __builtin_nontemporal_store(acc[d], reinterpret_cast<v2f*>(Yp + (int64_t)(b0 + d) * kN));
-#else
-#pragma unroll
-  for (int d = 0; d < BLK; ++d)
-    if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
-#endif
-}
-
 // The same sums with the Z window as a register ring indexed statically.  The p loop is unrolled by
 // the ring size R = BLK + PF - 1, so the slot (m - b0) mod R of block m is a compile-time register
 // at every unrolled step and the window never shifts (no v_mov).  After step p's products, block
@@ -246,7 +163,7 @@ __global__ void __launch_bounds__(kNT) upols_mac_kernel(const float2* __restrict
 // one read the zero spectra of out-of-range descriptors (G_q, q >= Q; Z_m, m < 0) and add exact
 // zeros.  grid (N/256, ceil(nb/BLK), npairs)
 template <int BLK, int PF, int GR>
-__global__ void __launch_bounds__(kNT, UPOLS_RING_WAVES) upols_mac_ring_kernel(const float2* __restrict__ X,
+__global__ void __launch_bounds__(kNT) upols_mac_ring_kernel(const float2* __restrict__ X,
                                                              const float2* __restrict__ Hs,
                                                              int64_t h_pair_stride, int nb, int Q,
                                                              float2* __restrict__ Y) {
@@ -320,17 +237,8 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
   const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
   const float2* in = Y + ((int64_t)pair * nb + b) * kN;
   float2 v[16];
-#ifdef DDSP_INV_NT  // A/B: streaming loads of Y
-  typedef float f2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(in + j + 256 * r));
-    v[r] = make_float2(t.x, t.y);
-  }
-#else
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = in[j + 256 * r];
-#endif
   fft4096<true>(v, lds);
   int ra, rb;
   pair_rows(pair, rows, pairing, ra, rb);
@@ -341,13 +249,8 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
     const int64_t s = (int64_t)b * kP + j + 256 * r - kP;
     if (s < T) {
       const int64_t so = reverse ? T - 1 - s : s;
-#ifdef DDSP_INV_YNT  // A/B: streaming stores of the output
-      __builtin_nontemporal_store(v[r].x, ya + so);
-      if (yb) __builtin_nontemporal_store(v[r].y, yb + so);
-#else
       ya[so] = v[r].x;
       if (yb) yb[so] = v[r].y;
-#endif
     }
   }
 }
@@ -417,46 +320,6 @@ __global__ void __launch_bounds__(64 * kCorrSlices) upols_corr_kernel(const floa
   }
 }
 
-// V_j = (-1)^f sum_q conj(G_q) GZ_{j+q} for BLK consecutive j (the inverse kernel's second half of
-// F^-1(V_j) is dx_j).  grid (N/256, ceil(nb/BLK), npairs)
-template <int BLK>
-__global__ void __launch_bounds__(kNT) upols_mac_adj_kernel(const float2* __restrict__ G,
-                                                            const float2* __restrict__ Hs, int nb, int Q,
-                                                            float2* __restrict__ V) {
-  const int f = blockIdx.x * kNT + threadIdx.x;
-  const int j0 = blockIdx.y * BLK;
-  const int pair = blockIdx.z;
-  const float2* Gp = G + (int64_t)pair * nb * kN + f;
-  const float2* Hp = Hs + f;
-  const float2 zero = make_float2(0.f, 0.f);
-  float2 win[BLK];
-  v2f acc[BLK];
-#pragma unroll
-  for (int d = 0; d < BLK; ++d) {
-    acc[d] = (v2f){0.f, 0.f};
-    const float2 gv = Gp[(int64_t)min(j0 + d, nb - 1) * kN];
-    win[d] = j0 + d < nb ? gv : zero;  // win[d] = GZ_{j0+d+q}
-  }
-  const int qmax = min(Q, nb - j0);
-#pragma unroll 4
-  for (int q = 0; q < qmax; ++q) {
-    const float2 h = Hp[(int64_t)q * kN];
-    const v2f hc = {h.x, -h.y}, hcr = {h.y, h.x};  // conj(h) and its rotation
-#pragma unroll
-    for (int d = 0; d < BLK; ++d) cmac(acc[d], win[d], hc, hcr);
-#pragma unroll
-    for (int d = 0; d < BLK - 1; ++d) win[d] = win[d + 1];
-    const int kn = j0 + BLK + q;
-    const float2 gv = Gp[(int64_t)min(kn, nb - 1) * kN];
-    win[BLK - 1] = kn < nb ? gv : zero;
-  }
-  const float sgn = (f & 1) ? -1.0f : 1.0f;
-  float2* Vp = V + (int64_t)pair * nb * kN + f;
-#pragma unroll
-  for (int d = 0; d < BLK; ++d)
-    if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(sgn * acc[d].x, sgn * acc[d].y);
-}
-
 // The adjoint MAC on the forward MAC's register ring: the window over GZ_{j0+d+q} (d < BLK) slides
 // forward, so block m sits in slot (m - j0) mod R (R = BLK + PF - 1), step u of a round reads slot
 // (d + u) mod R, and after its products block j0 + q + BLK + PF - 1 is loaded into the slot step q
@@ -476,17 +339,13 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* _
   const int voff = f * (int)sizeof(float2);
   float2 ring[R], g[GR];
   v2f acc[BLK];
-#ifndef DDSP_ADJ_ZAUX  // A/B: cache policy of the adjoint MAC's loads (as DDSP_MAC_ZAUX / _GAUX)
-#define DDSP_ADJ_ZAUX 0
-#endif
-#ifndef DDSP_ADJ_HAUX
-#define DDSP_ADJ_HAUX 0
-#endif
+  // default cache policy: the forward MAC's non-temporal bits slowed the train step here
+  // (0.556 -> 0.565-0.571 ms)
   auto zload = [&](int m, float2& dst) {
-    dst = row_load<DDSP_ADJ_ZAUX>(Grow + (int64_t)min(m, nb - 1) * kN, m < nb ? kRow : 0, voff);
+    dst = row_load<0>(Grow + (int64_t)min(m, nb - 1) * kN, m < nb ? kRow : 0, voff);
   };
   auto hload = [&](int q, float2& dst) {
-    dst = row_load<DDSP_ADJ_HAUX>(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff);
+    dst = row_load<0>(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff);
   };
 #pragma unroll
   for (int d = 0; d < BLK; ++d) {
@@ -609,23 +468,16 @@ int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* s
   const int64_t nb = upols_blocks(n);
   const int64_t Q = upols_kernel_windows(std::min(klen, n));
   const int64_t h_stride = per_row_kernel ? upols_kernel_windows(klen) * kN : 0;
-  constexpr int BLK = UPOLS_MAC_BLK;
-  if (nb > INT32_MAX || npairs > 65535 || (nb + BLK - 1) / BLK > 65535) return DDSP_HIP_EINVAL;
-  // UPOLS_MAC_BLK (25) output blocks per thread: each Z row is re-read (Q+BLK-1)/BLK times through L2
+  constexpr int RB = kRingBlk;
+  if (nb > INT32_MAX || npairs > 65535 || (nb + RB - 1) / RB > 65535) return DDSP_HIP_EINVAL;
+  // kRingBlk (25) output blocks per thread: each Z row is re-read (Q+BLK-1)/BLK times through L2
   // (A/B at config 2: 25 blocks 26.6 us vs 16 blocks 28.3 us, 8 and 32 no better; measured slower:
   // an LDS-tiled variant that reads Z once, 25%: lower occupancy, exposed loads; every operand
   // loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one thread per (pair, bin)
   // streaming all blocks with a register ring, 8%)
-#if UPOLS_MAC_RING
-  constexpr int RB = UPOLS_RING_BLK;
-  hipLaunchKernelGGL((upols_mac_ring_kernel<RB, UPOLS_RING_PF, UPOLS_RING_GR>),
+  hipLaunchKernelGGL((upols_mac_ring_kernel<RB, kRingPF, kRingGR>),
                      dim3(kN / kNT, (unsigned)((nb + RB - 1) / RB), (unsigned)npairs), dim3(kNT), 0, S(stream), Z,
                      reinterpret_cast<const float2*>(spectrum), h_stride, (int)nb, (int)Q, Y);
-#else
-  hipLaunchKernelGGL(upols_mac_kernel<BLK>, dim3(kN / kNT, (unsigned)((nb + BLK - 1) / BLK), (unsigned)npairs),
-                     dim3(kNT), 0, S(stream), Z, reinterpret_cast<const float2*>(spectrum), h_stride,
-                     (int)nb, (int)Q, Y);
-#endif
   int st = launch_status();
   if (st) return st;
   hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream),
@@ -642,23 +494,6 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   if (nb > INT32_MAX || npairs > 65535) return DDSP_HIP_EINVAL;
   float2* X = reinterpret_cast<float2*>(ws);
   float2* Y = X + (size_t)npairs * nb * kN;
-#ifdef DDSP_PROBE_REVERB_ONLY  // timing probe (tools/exp_cache.py, exp_gap.py): a subset of the reverb's kernels
-  // 1 forward, 2 MAC + inverse, 3 forward + MAC, 4 forward + inverse, 5 MAC, 6 inverse,
-  // 7 forward into the Y buffer + MAC from the (stale) X: both kernels, no fresh data between them
-  constexpr int PR = DDSP_PROBE_REVERB_ONLY;
-  if (PR == 1 || PR == 3 || PR == 4) launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
-  if (PR == 7) launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, Y, stream);
-  if (PR == 2) return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
-  if (PR == 3 || PR == 5 || PR == 7)
-    hipLaunchKernelGGL((upols_mac_ring_kernel<UPOLS_RING_BLK, UPOLS_RING_PF, UPOLS_RING_GR>),
-                       dim3(kN / kNT, (unsigned)((nb + UPOLS_RING_BLK - 1) / UPOLS_RING_BLK), (unsigned)npairs), dim3(kNT),
-                       0, S(stream), X, reinterpret_cast<const float2*>(spectrum), (int64_t)0, (int)nb,
-                       (int)upols_kernel_windows(std::min(klen, n)), Y);
-  if (PR == 4 || PR == 6)
-    hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), Y, (int)nb,
-                       n, (int)rows, (int)pairing, (int)reverse, y, n);
-  return launch_status();
-#endif
   // Z_b = FFT([x_b, 0])
   int st = launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
   if (st) return st;
@@ -685,7 +520,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   const int64_t groups = corr_groups(npairs);
   const bool need_x = dimp && !x_spectra;
   if (!ws || ws_bytes < upols_backward_workspace_bytes(rows, n, klen, !need_x)) return DDSP_HIP_EWORKSPACE;
-  if (nb > INT32_MAX || npairs > 65535 || Q > 65535 || (nb + 15) / 16 > 65535) return DDSP_HIP_EINVAL;
+  if (nb > INT32_MAX || npairs > 65535 || Q > 65535 || (nb + kRingBlk - 1) / kRingBlk > 65535) return DDSP_HIP_EINVAL;
   const size_t sb = upols_spectra_bytes(rows, n);
   char* w = reinterpret_cast<char*>(ws);
   float2* GZ = reinterpret_cast<float2*>(w);
@@ -697,15 +532,10 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   int st = launch_forward(g, n, rows, 1, nb, npairs, -1, 1, 0, GZ, stream);
   if (st) return st;
   if (dx) {
-#if UPOLS_MAC_RING
-    constexpr int AB = UPOLS_RING_BLK;
-    hipLaunchKernelGGL((upols_mac_adj_ring_kernel<AB, UPOLS_RING_PF, UPOLS_RING_GR>),
+    constexpr int AB = kRingBlk;
+    hipLaunchKernelGGL((upols_mac_adj_ring_kernel<AB, kRingPF, kRingGR>),
                        dim3(kN / kNT, (unsigned)((nb + AB - 1) / AB), (unsigned)npairs), dim3(kNT), 0, S(stream), GZ,
                        reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
-#else
-    hipLaunchKernelGGL(upols_mac_adj_kernel<16>, dim3(kN / kNT, (unsigned)((nb + 15) / 16), (unsigned)npairs),
-                       dim3(kNT), 0, S(stream), GZ, reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
-#endif
     if ((st = launch_status())) return st;
     hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), V,
                        (int)nb, n, (int)rows, 1, 0, dx, n);

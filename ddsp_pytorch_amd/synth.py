@@ -46,10 +46,6 @@ class SynthPath(nn.Module):
             self.reverb = Reverb(reverb_length, sample_rate)
             torch.random.set_rng_state(state)
         self.timer = None  # optional callable(name) -> context manager, used by bench.py
-        # True: the synthesis launch writes the reverb's input spectra (core.synth_reverb: no dry signal in
-        # HBM, no forward-transform launch).  Off by default: measured slower than the two launch groups
-        # (step 233 vs 214 us at config 2)
-        self.fused_reverb = False
 
     def _t(self, name):
         if self.timer is None:
@@ -75,21 +71,6 @@ class SynthPath(nn.Module):
 
     @torch.no_grad()
     def forward(self, f0, param, mags, noise=None):
-        if self.reverb is not None and self.fused_reverb:
-            if self.noise_mode == "inject" and noise is None:
-                raise ValueError("noise_mode='inject' needs a noise tensor")
-            nz = noise if self.noise_mode == "inject" else None
-            with self._t("synth_frames"):
-                z = core.synth_reverb_spectra(f0, param, mags, self.block_size, self.sample_rate,
-                                              bias=self.initial_bias, noise=nz)
-            if isinstance(z, torch.Tensor):
-                T = f0.shape[1] * self.block_size
-                spec = self.reverb._spectrum(T)
-                with self._t("reverb"):
-                    return core.reverb_apply_spectra(z, spec, self.reverb.length, f0.shape[0], T)
-            if z is not None:  # outside the fused transform's envelope: the dry signal, then the reverb
-                with self._t("reverb"):
-                    return self.reverb(z[1])
         signal = self.synthesize(f0, param, mags, noise)
         if self.reverb is not None:
             with self._t("reverb"):

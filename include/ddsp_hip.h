@@ -140,22 +140,6 @@ int ddsp_hip_synth_frames(const float* f0, const float* param, const float* raw_
                           int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
                           void* stream);
 
-/* Launch shape of ddsp_hip_synth_frames* for many frames (>= 2 x CUs x per_cu): per_cu persistent
- * workgroups per compute unit, each a preparation wave (controls, filter design, noise of the next
- * frame) beside the synthesis waves of the current one; 0 selects one workgroup per frame for every
- * launch; -1 restores the default (DDSP_HIP_PERSIST_WPC, else 0).  Process-wide (an atomic; safe from
- * any thread, applies to later launches); returns the previous setting. */
-int ddsp_hip_set_persistent_workgroups(int per_cu);
-
-/* Launch form of ddsp_hip_synth_frames* for many frames (the one-workgroup-per-frame shape): 1 = two
- * launches, the frames' controls, filter design and phase prefixes into a per-frame table first (one
- * wave per frame; a library-owned device buffer per stream), then the synthesis reading it; 0 = one
- * launch doing both per frame; -1 restores the default (DDSP_HIP_FRAME_TABLE, else 0: the two launches
- * measured slower).  Results are
- * bit-identical either way.  Launches on a stream that is capturing a graph always take one launch.
- * Process-wide (an atomic); returns the previous setting. */
-int ddsp_hip_set_frame_table(int on);
-
 /* ddsp_hip_synth_frames that also writes the controls DDSPDecoder.forward returns
  * (decoder.py:127-135: output['harmonic_ctrls'], output['noise_ctrls']) into controls_out (nullable),
  * laid out as [amplitudes B*F | harmonic_distribution B*F*H | magnitudes B*F*NB]: amplitudes =
@@ -169,34 +153,6 @@ int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t 
                                    uint64_t offset, float* out, float* harmonic_out, float* noise_out,
                                    float* controls_out, int64_t batch, int64_t frames, int64_t n_harmonic,
                                    int64_t n_bands, int64_t block_size, float sample_rate, void* stream);
-
-/* The synthesis section and the reverb in one call (decoder.py:106-125: harmonic + filtered noise
- * -> signal, then Reverb.forward, modules.py:28-35, whose IR spectrum comes from
- * ddsp_hip_reverb_spectrum for n_samples = frames * block_size): out[batch, frames*block_size] =
- * reverb(harmonic + noise).  The dry signal is never written: the synthesis kernel transforms each
- * 2048-sample block of two rows itself (the partitioned convolution's input spectra), then the
- * multiply-accumulate and inverse kernels of ddsp_hip_reverb_apply run.  Arguments as
- * ddsp_hip_synth_frames_controls; workspace >= ddsp_hip_synth_reverb_workspace_size.  Returns
- * DDSP_HIP_ERANGE outside its envelope (block_size must divide 2048, 256..1024): callers then run
- * ddsp_hip_synth_frames and ddsp_hip_reverb_apply. */
-size_t ddsp_hip_synth_reverb_workspace_size(int64_t batch, int64_t frames, int64_t block_size);
-/* The two halves of ddsp_hip_synth_reverb: the synthesis launch that writes the input-block spectra
- * (spectra_bytes >= ddsp_hip_reverb_input_spectra_bytes(batch, frames*block_size); DDSP_HIP_ERANGE
- * outside the envelope), and the reverb from those spectra (modules.py:28-35 after its forward
- * transform; workspace >= ddsp_hip_reverb_input_spectra_bytes). */
-int ddsp_hip_synth_reverb_spectra(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
-                                  int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed, uint64_t offset,
-                                  float* spectra, size_t spectra_bytes, int64_t batch, int64_t frames,
-                                  int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
-                                  void* stream);
-int ddsp_hip_reverb_apply_spectra(const float* input_spectra, const float* spectrum, float* out, int64_t batch,
-                                  int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
-                                  void* stream);
-int ddsp_hip_synth_reverb(const float* f0, const float* param, int64_t param_ld, const float* raw_magnitudes,
-                          int64_t magnitudes_ld, float bias, const float* noise, uint64_t seed, uint64_t offset,
-                          const float* spectrum, int64_t ir_length, float* out, void* workspace,
-                          size_t workspace_bytes, int64_t batch, int64_t frames, int64_t n_harmonic, int64_t n_bands,
-                          int64_t block_size, float sample_rate, void* stream);
 
 /* ddsp_hip_synth_frames for a stream of calls replayed from a captured HIP graph (the ddsp~
  * realtime host, realtime/ddsp_tilde/ddsp_model.cpp:32-52, calling the exported model once per

@@ -20,10 +20,7 @@ LIB = os.path.join(ROOT, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")
 # which are latency-bound: reported, not pinned.
 PINNED = ("synth_frame_kernelILb1ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0EE",
           "synth_frame_kernelILb1ELb0ELb1EE", "synth_frame_kernelILb0ELb0ELb1EE",
-          "synth_persist_kernelILb1ELb0ELb0ELb0EE", "synth_persist_kernelILb0ELb0ELb0ELb0EE",
-          "frame_backward_kernelILi2ELi0ELb0EE", "frame_backward_kernelILi1ELi0ELb0EE",
-          "synth_forward_kernelILb1ELb0EE", "synth_forward_kernelILb0ELb0EE",
-          "synth_tab_kernelILb1ELb1EE", "synth_tab_kernelILb0ELb1EE")
+          "frame_backward_kernelILi2ELi0ELb0EE", "frame_backward_kernelILi1ELi0ELb0EE")
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libddsp_hip.so not built (make)")

@@ -90,9 +90,7 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
 SHIPPED = ("synth_frame_kernelILb1ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0EE",
            "synth_frame_kernelILb1ELb1ELb0EE", "synth_frame_kernelILb0ELb1ELb0EE",
            "synth_frame_kernelILb1ELb0ELb1EE", "synth_frame_kernelILb0ELb0ELb1EE",
-           "synth_persist_kernelILb1ELb0ELb0ELb0EE", "synth_persist_kernelILb0ELb0ELb0ELb0EE",
-           "frame_backward_kernelILi2ELi2ELb1EE", "synth_forward_kernelILb1ELb0EE", "synth_forward_kernelILb0ELb0EE",
-           "synth_tab_kernelILb1ELb1EE", "synth_tab_kernelILb0ELb1EE")
+           "frame_backward_kernelILi2ELi2ELb1EE")
 
 
 def report(so, kern):
