@@ -7,7 +7,8 @@ Drop-in for hugofloresgarcia/ddsp_pytorch's synthesis hot path:
 * module level — ``ddsp_pytorch_amd.modules``: HarmonicSynth, FilteredNoise, Reverb
   (ddsp/models/modules.py), fused kernels;
 * ``install(ddsp)`` rebinds both inside an imported reference package;
-* ``DDSPDecoder`` — the reference model (same state_dict) running on these kernels.
+* ``DDSPDecoder`` and ``DDSPAutoencoder`` — the reference's two models (same state_dicts) running
+  on these kernels.
 
 All compute goes through the C-ABI library (include/ddsp_hip.h, lib/libddsp_hip.so);
 nothing falls back to CPU.
@@ -16,6 +17,7 @@ from . import core
 from .core import (amp_to_impulse_response, fft_convolve, harmonic_synth, remove_above_nyquist,
                    scale_function, upsample)
 from .decoder import DDSPDecoder
+from .encoder import DDSPAutoencoder
 from .install import install
 from .modules import FilteredNoise, HarmonicSynth, Reverb
 

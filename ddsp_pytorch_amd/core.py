@@ -397,8 +397,11 @@ def synth_frames(f0, param, mags, block_size, sample_rate, bias=-5.0, noise=None
 
 def _frame_rows(t):
     """(tensor, row stride) for a [B, F, C] tensor read row by row: unit stride on C and one row stride
-    over (B, F) — a column slice of a wider projection output qualifies as it is — else a contiguous copy."""
-    if t.dim() == 3 and t.stride(-1) == 1 and t.stride(0) == t.shape[1] * t.stride(1):
+    over (B, F) — a column slice of a wider projection output qualifies as it is — else a contiguous copy
+    (broadcast rows, stride 0, and overlapping rows included).  The kernels read these rows with scalar
+    loads only (no 16-byte vector loads), so a view's row base needs no more than 4-byte alignment."""
+    if (t.dim() == 3 and t.stride(-1) == 1 and t.stride(1) >= max(t.shape[-1], 1)
+            and t.stride(0) == t.shape[1] * t.stride(1)):
         return t, t.stride(1)
     t = t.contiguous()
     return t, t.shape[-1]

@@ -25,18 +25,22 @@ def mlp(in_size, hidden_size, n_layers):
 
 
 class GRUDecoder(nn.Module):
-    """ddsp/models/decoder.py:9-68 (z_dim=None form)."""
+    """ddsp/models/decoder.py:9-68, incl. the optional z conditioning (z_dim: a z_mlp whose output joins
+    the GRU input, decoder.py:31-39) that DDSPAutoencoder uses."""
 
-    def __init__(self, hidden_size: int):
+    def __init__(self, hidden_size: int, z_dim: int = None):
         super().__init__()
         self.register_buffer("cache_gru", torch.zeros(1, 1, hidden_size))
         self.f0_mlp = mlp(1, hidden_size, 3)
         self.loudness_mlp = mlp(1, hidden_size, 3)
-        self.gru = nn.GRU(2 * hidden_size, hidden_size, batch_first=True)
+        self.add_z = z_dim is not None
+        if self.add_z:
+            self.z_mlp = mlp(z_dim, hidden_size, 3)
+        self.gru = nn.GRU((3 if self.add_z else 2) * hidden_size, hidden_size, batch_first=True)
         self.out_mlp = mlp(hidden_size + 2, hidden_size, 3)
 
-    def forward(self, f0, loudness, realtime: bool = False):
-        return gru_decoder_forward(self, f0, loudness, None, realtime)
+    def forward(self, f0, loudness, z=None, realtime: bool = False):
+        return gru_decoder_forward(self, f0, loudness, z, realtime)
 
 
 def _gru(mod, hidden, h0):
@@ -70,25 +74,58 @@ def _hooked(m):
                 _m._global_forward_pre_hooks or type(m).forward is not torch.nn.Linear.forward)
 
 
+def _synth_overridden(m, cls):
+    """The synth module's calls must stay module calls: forward (pre-)hooks on it or globally, or a class
+    whose forward / get_controls is not this package's (``cls``; install() binds the same functions to
+    the reference's classes, so an installed reference module is not overridden)."""
+    from torch.nn.modules import module as _m
+    if m._forward_hooks or m._forward_pre_hooks or _m._global_forward_hooks or _m._global_forward_pre_hooks:
+        return True
+    t = type(m)
+    return any(getattr(t, n, None) is not cls.__dict__[n] for n in ("forward", "get_controls"))
+
+
+def _shared_projection(self):
+    """(W, b): the two projections' weights and biases as ONE contiguous [H+1+NB, hidden] matrix and
+    [H+1+NB] vector whose row slices ARE harmonic_proj's and noise_proj's parameters (their ``.data``
+    point into it).  Every read is live — in-place updates through ``.data``, load_state_dict or an
+    optimizer step land in the shared storage — and the single GEMM needs no per-call concatenation.
+    The sharing is (re-)established whenever a parameter no longer views it (a fresh module, ``.to()``,
+    a replaced ``.data``): the current values are copied into a new shared buffer first."""
+    hp, npj = self.harmonic_proj, self.noise_proj
+    h1 = hp.out_features
+    cached = self.__dict__.get("_proj_shared")
+    if cached is not None:
+        w, b = cached
+        if (w.device == hp.weight.device and w.dtype == hp.weight.dtype and
+                w.shape == (h1 + npj.out_features, hp.in_features) and hp.in_features == npj.in_features and
+                hp.weight.data_ptr() == w.data_ptr() and npj.weight.data_ptr() == w[h1:].data_ptr() and
+                hp.bias.data_ptr() == b.data_ptr() and npj.bias.data_ptr() == b[h1:].data_ptr() and
+                hp.weight.stride() == w.stride() and npj.weight.stride() == w.stride() and
+                hp.weight.shape == w[:h1].shape and npj.weight.shape == w[h1:].shape):
+            return w, b
+    with torch.no_grad():
+        w = torch.cat([hp.weight, npj.weight]).contiguous()
+        b = torch.cat([hp.bias, npj.bias]).contiguous()
+    hp.weight.data, npj.weight.data = w[:h1], w[h1:]
+    hp.bias.data, npj.bias.data = b[:h1], b[h1:]
+    self.__dict__["_proj_shared"] = (w, b)
+    return w, b
+
+
 def decoder_projections(self, hidden):
     """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE GEMM over the
-    concatenated weights (the two outputs are column slices of it; the fused synthesis kernel reads them
-    with their row stride).  The concatenated weights are cached while the four parameters are unchanged
-    (keyed on their storage and version counters, like Reverb's spectrum)."""
+    two projections' weights held in one shared buffer (``_shared_projection``; the two outputs are column
+    slices of it, which the fused synthesis kernel reads with their row stride).  Under autograd the
+    concatenation is differentiable, so the parameters receive their gradients as the reference's do."""
     hp, npj = self.harmonic_proj, self.noise_proj
     if not hidden.is_cuda or hp.bias is None or npj.bias is None or _hooked(hp) or _hooked(npj):
         return hp(hidden), npj(hidden)  # (module hooks see the calls the reference makes)
     ps = (hp.weight, hp.bias, npj.weight, npj.bias)
-    key = tuple((p.data_ptr(), p._version) for p in ps)
-    cache = self.__dict__.get("_proj_cat")
     if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
         w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
-    elif cache is not None and cache[0] == key:
-        w, b = cache[1], cache[2]
     else:
-        with torch.no_grad():
-            w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])
-        self.__dict__["_proj_cat"] = (key, w, b)
+        w, b = _shared_projection(self)
     out = torch.nn.functional.linear(hidden, w, b)
     h1 = hp.out_features
     return out[..., :h1], out[..., h1:]
@@ -106,7 +143,8 @@ def decoder_synthesize(self, hidden, f0):
     param, mags = decoder_projections(self, hidden)
     H, NB, bs = param.shape[-1] - 1, mags.shape[-1], int(hs.block_size)
     fused = (param.is_cuda and int(ns.block_size) == bs and param.shape[0] <= 65535
-             and core.synth_frames_in_envelope(H, NB, bs, param.shape[0]))
+             and core.synth_frames_in_envelope(H, NB, bs, param.shape[0])
+             and not _synth_overridden(hs, HarmonicSynth) and not _synth_overridden(ns, FilteredNoise))
     if fused:
         mode = getattr(ns, "noise_mode", "torch")
         if mode not in NOISE_MODES:

@@ -6,7 +6,7 @@ package attributes redirects every caller.  Module level: the reference classes'
 forwards are replaced by the fused ones (same instance attributes and parameters).
 ``uninstall()`` restores everything.
 """
-from . import core, decoder, modules
+from . import core, decoder, encoder, modules
 
 FUNCTIONS = ("scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
              "amp_to_impulse_response", "fft_convolve")
@@ -69,6 +69,15 @@ def install(pkg=None, functions=True, module_forwards=True):
         ref_decoder_mod = getattr(pkg.models, "decoder", None)
         for cls_name, fn in (("GRUDecoder", decoder.gru_decoder_forward), ("DDSPDecoder", decoder.decoder_forward)):
             ref_cls = getattr(ref_decoder_mod, cls_name, None)
+            if ref_cls is not None:
+                saved_methods[(ref_cls, "forward")] = ref_cls.__dict__.get("forward")
+                setattr(ref_cls, "forward", fn)
+        # the second caller, DDSPAutoencoder.forward (encoder.py:63-103): the same fused synthesis
+        # section after its MFCC encoder (whose GRU, encoder.py:19-25, runs on the step kernel too)
+        ref_encoder_mod = getattr(pkg.models, "encoder", None)
+        for cls_name, fn in (("MFCCEncoder", encoder.mfcc_encoder_forward),
+                             ("DDSPAutoencoder", encoder.autoencoder_forward)):
+            ref_cls = getattr(ref_encoder_mod, cls_name, None)
             if ref_cls is not None:
                 saved_methods[(ref_cls, "forward")] = ref_cls.__dict__.get("forward")
                 setattr(ref_cls, "forward", fn)

@@ -16,6 +16,7 @@ computed by the reference's own functions and modules:
                              harmonic_synth, amp_to_impulse_response, fft_convolve
 * ``ddsp/models/modules.py:7-128``  Reverb, HarmonicSynth, FilteredNoise
 * ``ddsp/models/decoder.py:76-136`` DDSPDecoder.forward
+* ``ddsp/models/encoder.py:31-103`` DDSPAutoencoder.forward (MFCC encoder + z-conditioned decoder)
 
 Inputs follow SURVEY.md §8(d): f0 = 50*20**U[0,1) Hz, raw controls N(0,1),
 noise U[-1,1) drawn by ``torch.rand`` after ``torch.manual_seed(123)``, reverb
@@ -193,6 +194,7 @@ def main():
 
     grad_goldens(ddsp, decoder, modules, sr)
     realtime_goldens(decoder, sr)
+    autoencoder_golden(sr)
 
 
 @torch.no_grad()
@@ -289,6 +291,30 @@ def grad_goldens(ddsp, decoder, modules, sr):
     masked_loss_golden(ddsp)
 
 
+@torch.no_grad()
+def autoencoder_golden(sr):
+    """g9: the reference's second caller of the path, DDSPAutoencoder.forward (encoder.py:63-103): the
+    MFCC encoder (LayerNorm -> GRU -> Linear to z, encoder.py:12-28), the z-conditioned GRUDecoder
+    (decoder.py:11-66), then the same synthesis section as DDSPDecoder.forward.  Small hidden size,
+    seeded; the MFCCs are an input tensor (the encoder needs no librosa)."""
+    from ddsp.models import encoder
+    torch.manual_seed(0)
+    model = encoder.DDSPAutoencoder(32, 100, 65, sr, 512, True).eval()
+    f0, loudness, _, _ = synth_inputs(9, 2, 16, 100, 65)
+    mfcc = torch.randn(2, 16, 30, generator=torch.Generator().manual_seed(19)) * 10.0
+    torch.manual_seed(123)
+    noise_in = torch.rand(2, 16, 512) * 2 - 1  # the draw FilteredNoise.forward makes next
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness, "mfcc": mfcc})
+    sd = {"sd." + k: v for k, v in model.state_dict().items()}
+    save("g9_autoencoder", hidden_size=32, n_harmonic=100, n_bands=65, sample_rate=sr, block_size=512,
+         pitch=f0, loudness=loudness, mfcc=mfcc, noise_in=noise_in, signal=o["signal"], noise=o["noise"],
+         harmonic_audio=o["harmonic_audio"], z=o["z"],
+         amplitudes=o["harmonic_ctrls"]["amplitudes"],
+         distribution=o["harmonic_ctrls"]["harmonic_distribution"],
+         magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
+
+
 def masked_loss_golden(ddsp):
     """g7b: train.py:70-76's loss restricted to the well-conditioned bins, on g7's signals, computed by
     the reference's multiscale_fft / safe_log (core.py:10-41) in fp32 with autograd.  The bins with
@@ -320,6 +346,10 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["g8"]:  # only the realtime fixture
         torch.set_num_threads(8)
         realtime_goldens(import_reference()[2], 48000)
+    elif sys.argv[1:] == ["g9"]:  # only the autoencoder fixture
+        torch.set_num_threads(8)
+        import_reference()
+        autoencoder_golden(48000)
     elif sys.argv[1:] == ["g7b"]:  # only the masked-loss fixture (reads g7)
         torch.set_num_threads(8)
         masked_loss_golden(import_reference()[0])

@@ -1,0 +1,56 @@
+"""The decoder's fused route on the GPU reads live parameters and respects module hooks:
+an in-place ``.data`` update of a projection between two no_grad forwards changes the output exactly as
+a fresh model with those weights computes it; a forward hook on a synth module makes the module-by-module
+route run (the hook fires) with the same result."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dd():
+    import ddsp_pytorch_amd
+    return ddsp_pytorch_amd
+
+
+def _batch():
+    g = torch.Generator().manual_seed(3)
+    return {"pitch": (50.0 * 20.0 ** torch.rand(2, 8, 1, generator=g)).cuda(),
+            "loudness": torch.randn(2, 8, 1, generator=g).cuda()}
+
+
+def _run(m, batch):
+    with torch.no_grad():
+        torch.manual_seed(7)
+        return m(batch)["signal"]
+
+
+def test_inplace_data_update_is_seen(dd):
+    torch.manual_seed(0)
+    m = dd.DDSPDecoder(64, 20, 17, 48000, 256, True).cuda().eval()
+    batch = _batch()
+    a = _run(m, batch)
+    m.harmonic_proj.weight.data.mul_(1.5)   # no version bump
+    m.noise_proj.bias.data.add_(0.25)
+    b = _run(m, batch)
+    assert not torch.allclose(a, b)
+    fresh = dd.DDSPDecoder(64, 20, 17, 48000, 256, True)
+    fresh.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    c = _run(fresh.cuda().eval(), batch)
+    torch.testing.assert_close(b, c, rtol=0, atol=0)
+
+
+def test_hooked_synth_module_keeps_module_calls(dd):
+    torch.manual_seed(0)
+    m = dd.DDSPDecoder(64, 20, 17, 48000, 256, False).cuda().eval()
+    batch = _batch()
+    plain = _run(m, batch)
+    seen = []
+    h = m.harmonic_synth.register_forward_hook(lambda mod, i, o: seen.append(o.shape))
+    try:
+        hooked = _run(m, batch)
+    finally:
+        h.remove()
+    assert seen, "the hook did not fire: the fused route skipped the module call"
+    torch.testing.assert_close(hooked, plain, rtol=1e-5, atol=2e-6)

@@ -35,6 +35,7 @@ def _import_reference():
     if REF not in sys.path:
         sys.path.insert(0, REF)
     ddsp = importlib.import_module("ddsp")
+    importlib.import_module("ddsp.models.encoder")
     decoder = importlib.import_module("ddsp.models.decoder")
     modules = importlib.import_module("ddsp.models.modules")
     return ddsp, modules, decoder
@@ -174,3 +175,45 @@ def test_projection_hooks_keep_module_calls():
             return super().forward(x) * 2
 
     assert _hooked(Wrapped(4, 3))
+
+
+def test_install_routes_the_autoencoder():
+    """The reference's second caller of the path, DDSPAutoencoder.forward (encoder.py:63-103), and its
+    MFCCEncoder.forward are swapped by install() for this package's (the fused synthesis section after
+    the encoder and the z-conditioned decoder); every self.X they read resolves on real reference
+    instances; the swapped forward refuses CPU tensors; uninstall() restores both."""
+    ddsp, ref_modules, ref_decoder = _import_reference()
+    ref_encoder = importlib.import_module("ddsp.models.encoder")
+    import ddsp_pytorch_amd as dd
+    torch.manual_seed(0)
+    model = ref_encoder.DDSPAutoencoder(32, 8, 9, 48000, 64, True)
+    orig = {c: getattr(ref_encoder, c).__dict__["forward"] for c in ("DDSPAutoencoder", "MFCCEncoder")}
+    inst = dd.install(ddsp)
+    try:
+        assert ref_encoder.DDSPAutoencoder.__dict__["forward"] is dd.encoder.autoencoder_forward
+        assert ref_encoder.MFCCEncoder.__dict__["forward"] is dd.encoder.mfcc_encoder_forward
+        for fn in (dd.encoder.autoencoder_forward, dd.decoder.decoder_synthesize, dd.decoder.decoder_projections):
+            missing = {a for a in _self_reads(fn) if not hasattr(model, a)}
+            assert not missing, f"{fn.__name__} reads {missing}, absent on a reference DDSPAutoencoder"
+        missing = {a for a in _self_reads(dd.encoder.mfcc_encoder_forward) if not hasattr(model.encoder, a)}
+        assert not missing, missing
+        # the z-conditioned GRUDecoder of the reference takes the swapped forward's z path
+        guarded = []
+        missing = {a for a in _self_reads(dd.decoder.gru_decoder_forward, guarded) if not hasattr(model.decoder, a)}
+        assert not missing and all(hasattr(model.decoder, a) for a in guarded)
+        # on the host the encoder (plain torch) still computes the reference's z
+        mfcc = torch.randn(1, 4, 30)
+        with torch.no_grad():
+            z_ours = model.encoder(mfcc)
+        inst.uninstall()
+        with torch.no_grad():
+            z_ref = model.encoder(mfcc)
+        torch.testing.assert_close(z_ours, z_ref, rtol=1e-6, atol=1e-7)
+        inst = dd.install(ddsp)
+        batch = {"pitch": torch.full((1, 4, 1), 220.0), "loudness": torch.zeros(1, 4, 1), "mfcc": mfcc}
+        with pytest.raises(Exception):
+            model(batch)  # CPU tensors: the synthesis refuses (no CPU fallback)
+    finally:
+        inst.uninstall()
+    for c, f in orig.items():
+        assert getattr(ref_encoder, c).__dict__["forward"] is f
