@@ -26,7 +26,7 @@ __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
     "harmonic_synth_frames", "harmonic_synth_params", "synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
-    "reverb_spectrum", "reverb_apply", "set_noise_seed", "safe_log", "stft_magnitude", "multiscale_fft",
+    "reverb_spectrum", "reverb_impulse_spectrum", "reverb_apply", "set_noise_seed", "safe_log", "stft_magnitude", "multiscale_fft",
 ]
 
 
@@ -482,6 +482,19 @@ def reverb_spectrum(impulse, n_samples):
     L = h.numel()
     spec = torch.empty(reverb_spectrum_floats(n_samples, L), dtype=torch.float32, device=h.device)
     _lib.call("reverb_spectrum", _lib.ptr(h), L, int(n_samples), _lib.ptr(spec), _lib.stream_of(h))
+    return spec
+
+
+def reverb_impulse_spectrum(noise, decay, wet, sample_rate, n_samples):
+    """modules.py:21-35: Reverb.build_impulse and its partition spectra for n_samples in one launch
+    (equal to reverb_spectrum(reverb_build_impulse(...), n_samples) bit for bit).  No autograd: the
+    module's backward differentiates through noise/decay/wet itself."""
+    _dev(noise, decay, wet)
+    L = noise.shape[0]
+    n = _c(noise)
+    spec = torch.empty(reverb_spectrum_floats(n_samples, L), dtype=torch.float32, device=n.device)
+    _lib.call("reverb_impulse_spectrum", _lib.ptr(n), _lib.ptr(_c(decay)), _lib.ptr(_c(wet)), L,
+              float(sample_rate), int(n_samples), _lib.ptr(spec), _lib.stream_of(n))
     return spec
 
 

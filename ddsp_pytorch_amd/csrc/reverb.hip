@@ -133,6 +133,13 @@ int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const 
   return launch_status();
 }
 
+int ddsp_hip_reverb_impulse_spectrum(const float* noise, const float* decay, const float* wet, int64_t ir_length,
+                                     float sample_rate, int64_t n_samples, float* spectrum, void* stream) {
+  if (ir_length < 1 || n_samples < 1 || !noise || !decay || !wet || !spectrum || !(sample_rate > 0))
+    return DDSP_HIP_EINVAL;
+  return upols_impulse_spectrum(noise, decay, wet, std::min(ir_length, n_samples), sample_rate, spectrum, stream);
+}
+
 int ddsp_hip_reverb_spectrum(const float* impulse, int64_t ir_length, int64_t n_samples,
                              float* spectrum, void* stream) {
   if (ir_length < 1 || n_samples < 1 || !impulse || !spectrum) return DDSP_HIP_EINVAL;

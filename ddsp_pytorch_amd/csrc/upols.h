@@ -13,6 +13,9 @@ int64_t upols_blocks(int64_t n);
 size_t upols_spectrum_floats(int64_t krows, int64_t klen);
 size_t upols_workspace_bytes(int64_t rows, int64_t n, bool pairing);
 // spectra of krows kernels (row stride ld, first klen taps used), scaled by 1/N
+// spectra of Reverb.build_impulse(noise, decay, wet) cropped to klen taps, built in the same launch
+int upols_impulse_spectrum(const float* noise, const float* decay, const float* wet, int64_t klen, float sr,
+                           float* spectrum, void* stream);
 int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, float* spectrum,
                    void* stream);
 // y[rows, n] = (x[rows, n] (*) h)[0:n]; spectrum from upols_spectrum (one kernel shared by all

@@ -153,6 +153,40 @@ __global__ void __launch_bounds__(kNT) upols_kernel_spectrum_kernel(const float*
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
 }
 
+// Reverb.build_impulse (modules.py:21-26) fused into the IR's partition spectra (modules.py:30-35):
+// G[q][:] = FFT(imp[(q-1)P, (q+1)P)) / N with imp[i] = noise[i] exp(-softplus(-decay) t 500) sigmoid(wet),
+// t = fl32(i / sr), imp[0] = 1, zero at or past klen — the arithmetic of reverb.hip's
+// build_impulse_kernel per tap, so the spectra are those of upols_spectrum(build_impulse(...)) bit for bit.
+// One launch instead of two (the impulse never goes to HBM); grid (Q + 1)
+__global__ void __launch_bounds__(kNT) upols_impulse_spectrum_kernel(const float* __restrict__ noise,
+                                                                     const float* __restrict__ decay,
+                                                                     const float* __restrict__ wet, int64_t klen,
+                                                                     float sr, int QG, float2* __restrict__ Hs) {
+  __shared__ float2 lds[kPad];
+  const int q = blockIdx.x, j = threadIdx.x;
+  const float d = -decay[0];
+  const float sp = d > 20.0f ? d : log1pf(expf(d));  // softplus(-decay), torch's threshold 20
+  const float neg = -sp;
+  const float w = 1.0f / (1.0f + expf(-wet[0]));
+  const float inv_n = 1.0f / (float)kN;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = (int64_t)(q - 1) * kP + j + 256 * r;
+    float h = 0.0f;
+    if (s >= 0 && s < klen) {
+      const float t = (float)s / sr;
+      const float env = expf((neg * t) * 500.0f);
+      h = s == 0 ? 1.0f : (noise[s] * env) * w;
+    }
+    v[r] = make_float2(h * inv_n, 0.0f);
+  }
+  fft4096<false>(v, lds);
+  float2* out = Hs + (int64_t)q * kN;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+}
+
 // The same sums with the Z window as a register ring indexed statically.  The p loop is unrolled by
 // the ring size R = BLK + PF - 1, so the slot (m - b0) mod R of block m is a compile-time register
 // at every unrolled step and the window never shifts (no v_mov).  After step p's products, block
@@ -447,6 +481,15 @@ int upols_spectrum(const float* h, int64_t ld, int64_t klen, int64_t krows, floa
   if (QG > 65535 || krows > 65535) return DDSP_HIP_EINVAL;
   hipLaunchKernelGGL(upols_kernel_spectrum_kernel, dim3((unsigned)QG, (unsigned)krows), dim3(kNT), 0,
                      S(stream), h, ld, klen, (int)QG, reinterpret_cast<float2*>(spectrum));
+  return launch_status();
+}
+
+int upols_impulse_spectrum(const float* noise, const float* decay, const float* wet, int64_t klen, float sr,
+                           float* spectrum, void* stream) {
+  const int64_t QG = upols_kernel_windows(klen);
+  if (QG > 65535) return DDSP_HIP_EINVAL;
+  hipLaunchKernelGGL(upols_impulse_spectrum_kernel, dim3((unsigned)QG), dim3(kNT), 0, S(stream), noise, decay, wet,
+                     klen, sr, (int)QG, reinterpret_cast<float2*>(spectrum));
   return launch_status();
 }
 

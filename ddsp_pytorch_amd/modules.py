@@ -54,8 +54,9 @@ class Reverb(nn.Module):
         key = (n_samples, self.noise.device, self.noise.data_ptr(), self.noise._version,
                self.decay._version, self.wet._version, self.decay.data_ptr(), self.wet.data_ptr())
         if key != getattr(self, "_spec_key", None) or not getattr(self, "cache_spectrum", True):
-            with torch.no_grad():
-                self._spec = core.reverb_spectrum(self.build_impulse(), n_samples)
+            with torch.no_grad():  # build_impulse (modules.py:21-26) and its spectra: one launch
+                self._spec = core.reverb_impulse_spectrum(self.noise, self.decay, self.wet, self.sample_rate,
+                                                          n_samples)
             self._spec_key = key
         return self._spec
 

@@ -145,14 +145,19 @@ def chunk_bounds(batch, chunks):
 
 
 def synthesize_pipelined(synth, inputs, batch, tails, chunks=4, src=0, dst=0, group=None,
-                         device=None, dtype=torch.float32):
+                         device=None, dtype=torch.float32, trace=None):
     """Root-held batch through the sharded synth path with overlapped collectives.
 
     inputs: list of full-batch [batch, *tail] tensors on ``src`` (ignored elsewhere, may be
     None), in the order ``synth`` takes them; tails: their per-item shapes (every rank knows
     them).  Each of ``chunks`` pieces of the batch is scattered over the ranks, synthesised
     ([b, T, 1] per shard) and gathered on ``dst``.  Returns [batch, T, 1] on dst, None elsewhere.
+
+    ``trace`` (a list, optional) receives the order of events — ("scatter", c) issued, ("scattered", c)
+    waited, ("synth", c), ("gather", c) issued, ("gathered", c) waited — so tests can check the overlap:
+    scatter(c+1) is issued before synth(c) and no gather is waited before the last synth.
     """
+    log = trace.append if trace is not None else (lambda e: None)
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if batch < world:
@@ -163,6 +168,7 @@ def synthesize_pipelined(synth, inputs, batch, tails, chunks=4, src=0, dst=0, gr
 
     def start(c):
         a, b = bounds[c]
+        log(("scatter", c))
         return _scatter_async(packed[a:b] if packed is not None else None, b - a, cols, dtype,
                               device, src, group)
 
@@ -172,15 +178,19 @@ def synthesize_pipelined(synth, inputs, batch, tails, chunks=4, src=0, dst=0, gr
     for c in range(len(bounds)):
         work, recv, n = pending
         work.wait()
+        log(("scattered", c))
         if c + 1 < len(bounds):
             pending = start(c + 1)  # in flight while this chunk is synthesised
         audio = synth(*unpack_items(recv[:n], tails))
+        log(("synth", c))
         a, b = bounds[c]
         if rank == dst and result is None:  # every rank's audio has this item shape
             result = audio.new_empty((batch,) + tuple(audio.shape[1:]))
         gathers.append((a, _gather_async(audio, b - a, dst, group, into=result[a:b] if result is not None else None)))
-    for a, (work, recv, sizes) in gathers:
+        log(("gather", c))
+    for c, (a, (work, recv, sizes)) in enumerate(gathers):
         work.wait()
+        log(("gathered", c))
         if rank == dst and recv is not None:  # ragged shards: compact the padded blocks
             for r, (s0, s1) in zip(recv, sizes):
                 result[a + s0:a + s1].copy_(r[: s1 - s0])

@@ -178,6 +178,11 @@ int ddsp_hip_reverb_build_impulse(const float* noise, const float* decay, const 
  *   ddsp_hip_reverb_apply:   x[B,T] (*) IR -> out[B,T] using that spectrum. */
 size_t ddsp_hip_reverb_spectrum_floats(int64_t n_samples, int64_t ir_length);
 size_t ddsp_hip_reverb_workspace_size(int64_t batch, int64_t n_samples, int64_t ir_length);
+/* modules.py:21-35: Reverb.build_impulse and the IR's partition spectra (as ddsp_hip_reverb_spectrum of
+ * the built impulse, bit for bit) in ONE launch — the impulse is never written.  For a reverb whose
+ * parameters change every call (training: the reference rebuilds the IR in every Reverb.forward). */
+int ddsp_hip_reverb_impulse_spectrum(const float* noise, const float* decay, const float* wet, int64_t ir_length,
+                                     float sample_rate, int64_t n_samples, float* spectrum, void* stream);
 int ddsp_hip_reverb_spectrum(const float* impulse, int64_t ir_length, int64_t n_samples,
                              float* spectrum, void* stream);
 int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int64_t batch,

@@ -147,3 +147,70 @@ def test_pipelined_scatter_synth_gather(world, batch, chunks):
         res[k] = (v, shape)
     assert res["pipe"][0] < 1e-6 and res["pipe"][1][0] == batch, res
     assert all(res["none%d" % r][0] for r in range(1, world))
+
+
+def _pipeline_order_worker(rank, world, port, batch, chunks, q):
+    """Config-5-shaped items (F=400, H=128, NB=65, bs=512) through synthesize_pipelined at world 4.
+    The synth stand-in is cheap and item-local (the kernels cannot run here): audio row i is a fixed
+    function of item i's controls, so the gathered batch is checked item by item."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        F, H, NB, bs = 400, 128, 65, 512
+        tails = [(F, 1), (F, H + 1), (F, NB)]
+
+        def synth(f0, param, mags):  # [b, F*bs, 1], item-local
+            v = f0[:, :, 0] + param.sum(-1) - mags.sum(-1)
+            return v.repeat_interleave(bs, 1).unsqueeze(-1)
+
+        g = torch.Generator().manual_seed(5)
+        full = [torch.rand((batch,) + t, generator=g) for t in tails]
+        held = full if rank == 0 else None
+        trace = []
+        out = synthesize_pipelined(synth, held, batch, tails, chunks=chunks, trace=trace)
+        res = {"trace": trace}
+        if rank == 0:
+            res["err"] = float((out - synth(*full)).abs().max())
+            res["shape"] = tuple(out.shape)
+        else:
+            res["none"] = out is None
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chunks", [1, 4, 8])
+def test_pipelined_world4_config5_items_overlap_order(chunks):
+    """SURVEY §8(e) at world 4 with config-5-shaped items: the scatter of chunk c+1 is issued before
+    chunk c is synthesised, every gather is issued right after its synth and none is waited before the
+    last synth (the collectives of neighbouring chunks overlap the synthesis), and the gathered batch
+    equals the one-process result item for item."""
+    world, batch = 4, 32
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_order_worker, args=(r, world, port, batch, chunks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert res[0]["err"] == 0.0 and res[0]["shape"] == (batch, 400 * 512, 1)
+    assert all(res[r]["none"] for r in range(1, world))
+    n = len(chunk_bounds(batch, min(chunks, batch // world)))
+    assert n == min(chunks, batch // world)
+    for r in range(world):
+        tr = res[r]["trace"]
+        pos = {e: i for i, e in enumerate(tr)}
+        assert len(pos) == 5 * n, tr
+        last_synth = pos[("synth", n - 1)]
+        for c in range(n):
+            assert pos[("scattered", c)] < pos[("synth", c)] < pos[("gather", c)] < pos[("gathered", c)]
+            if c + 1 < n:
+                assert pos[("scatter", c + 1)] < pos[("synth", c)]   # next chunk's scatter in flight
+                assert pos[("gather", c)] < pos[("synth", c + 1)]    # this chunk's gather in flight
+            assert pos[("gathered", c)] > last_synth                 # no gather waited early
