@@ -60,6 +60,24 @@ def kernel_source_sha():
         return None
 
 
+def fir_macs_per_frame(n_bands, block_size):
+    """Multiply-adds of one frame's causal, truncated noise convolution (core.py:169-176 keeps the first
+    block_size outputs of signal (*) h): sum over the filter's nonzero taps m of (block_size - m).  The
+    taps follow amp_to_impulse_response (core.py:158-164): h[j] = ir[(q - n/2) mod n] * hann_n[q] with
+    q = (j + n/2) rolled into the block, zero where q >= n or hann_n[q] = 0 (q = 0).  At 65 bands and
+    block 512: taps [0, 64) and (448, 512) -> 64 x 512 MACs, i.e. n/2 = 64 per sample (the filter has
+    127 nonzero taps, but causality truncates the wrapped ones to the block's last samples)."""
+    n, half, bs = 2 * (n_bands - 1), n_bands - 1, block_size
+    total = 0
+    for j in range(bs):
+        q = j + half
+        if q >= bs:
+            q = q - bs if half < bs else q % bs
+        if 0 < q < n:
+            total += bs - j
+    return total
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -489,14 +507,21 @@ def scatter_gather_leg(synth, held, global_batch, tails, samples_per_step, steps
             g)
 
 
+PIPELINE_MIN_BATCHES = 200
+
+
 def pipelined_leg(syn, run_args, samples_per_step, steps, reverb_cus, dev, dist, warm=40):
     """Serving form over consecutive batches (synth.PipelinedSynthPath): the synthesis of batch i+1
     on one CU partition beside the reverb of batch i on the other.  Same work per batch as the
-    headline step; reported beside it, never as it.  Timed between barrier + device sync, max over
-    ranks; latency = one batch alone through both stages (best of 5).  The warmup runs until the
-    caching allocator holds the blocks the two streams cycle through (fresh blocks are hipMalloc'd
-    while signals still wait for the reverb stream: the first ~10-20 batches run slower)."""
+    headline step; reported beside it, never as it.  A steady-state rate: at least
+    PIPELINE_MIN_BATCHES batches are timed whatever --steps is (at the driver's 20 the pipeline's fill
+    and drain and the host's start-up dominate: 0.222 vs 0.189 ms per batch at 200, profiles/
+    r04c_pipelined_steps.log).  Timed between barrier + device sync, max over ranks; latency = one batch
+    alone through both stages (best of 5).  The warmup runs until the caching allocator holds the
+    blocks the two streams cycle through (fresh blocks are hipMalloc'd while signals still wait for
+    the reverb stream: the first ~10-20 batches run slower)."""
     from ddsp_pytorch_amd.synth import PipelinedSynthPath
+    steps = max(int(steps), PIPELINE_MIN_BATCHES)
     pipe = PipelinedSynthPath(syn, reverb_cus=reverb_cus, device=dev)
     for _ in range(warm):
         pipe(*run_args)
@@ -521,7 +546,7 @@ def pipelined_leg(syn, run_args, samples_per_step, steps, reverb_cus, dev, dist,
         pipe.join()
         _sync(dev)
         lat.append(time.perf_counter() - t1)
-    return {"value": round(samples_per_step * steps / t, 1), "unit": "samples/s",
+    return {"value": round(samples_per_step * steps / t, 1), "unit": "samples/s", "batches_timed": steps,
             "ms_per_step": round(t / steps * 1e3, 4), "latency_ms": round(min(lat) * 1e3, 4),
             "cu_split": {"reverb": reverb_cus, "synthesis": pipe.n_cu - reverb_cus},
             "note": "two-stage pipeline over consecutive batches on CU-masked streams (synthesis of "
@@ -597,8 +622,10 @@ def main():
     for name in ("synth_frames", "reverb"):
         breakdown = EventTimer([name])
         syn.timer = breakdown
+        for _ in range(20):  # back at the loaded clock before the events are read
+            step()
         breakdown.enabled = True
-        for _ in range(min(args.steps, 50)):
+        for _ in range(50):
             step()
         torch.cuda.synchronize()
         breakdown.enabled = False
@@ -627,10 +654,13 @@ def main():
         slots = osc_slots
         slots_src = ("oscillator model only (" + ("the PMC counts were taken on another build of the kernel"
                      if stale else "no PMC counts for this configuration") + ")")
-    # algorithmic issue slots: per sample H x (6 VALU + v_sin_f32 at 4 slots) for the
-    # oscillator + 127 FIR taps (one FMA each) for the noise filter; no controls, RNG or addressing
-    fir_taps = 2 * (NB - 1) - 1
-    alg_slots = B * F * bs / 64 * (H * OSC_SLOTS_PER_SINE + fir_taps)
+    # algorithmic issue slots: per sample H x (6 VALU + v_sin_f32 at 4 slots) for the oscillator + the
+    # causal noise FIR's multiply-adds (one FMA each: n/2 = 64 per sample at 65 bands, fir_macs_per_frame);
+    # no controls, RNG or addressing.  Rounds 2-3 counted the filter's 127 nonzero taps for every sample
+    # (kept as frac_algorithmic_r03_convention for comparison)
+    fir_macs = fir_macs_per_frame(NB, bs) / bs
+    alg_slots = B * F * bs / 64 * (H * OSC_SLOTS_PER_SINE + fir_macs)
+    alg_slots_r03 = B * F * bs / 64 * (H * OSC_SLOTS_PER_SINE + 2 * (NB - 1) - 1)
     achieved = slots / (osc_ms * 1e-3)
     osc_bytes = 4 * (H + 2) * B * F * bs
     roofline = {"bound": "valu", "achieved": round(achieved / 1e12, 4), "peak": VALU_PEAK_SLOTS / 1e12,
@@ -638,8 +668,10 @@ def main():
                 "frac": round(achieved / VALU_PEAK_SLOTS, 4),
                 "frac_algorithmic": round(alg_slots / (osc_ms * 1e-3) / VALU_PEAK_SLOTS, 4),
                 "algorithmic_slots_per_launch": round(alg_slots),
-                "algorithmic_slots_note": f"samples/64 x (H x {OSC_SLOTS_PER_SINE} + {fir_taps}): per (sample, "
-                                          "harmonic) 6 VALU + v_sin_f32 (4 slots), per sample the 127-tap noise FIR",
+                "algorithmic_slots_note": f"samples/64 x (H x {OSC_SLOTS_PER_SINE} + {fir_macs:g}): per (sample, "
+                                          "harmonic) 6 VALU + v_sin_f32 (4 slots), per sample the causal noise "
+                                          "FIR's multiply-adds (bench.fir_macs_per_frame)",
+                "frac_algorithmic_r03_convention": round(alg_slots_r03 / (osc_ms * 1e-3) / VALU_PEAK_SLOTS, 4),
                 "valu_counts_kernel_sha": vc.get("kernel_sha"), "kernel_sha": src_sha,
                 "traffic": traffic.get("synth_frame_kernel"),
                 "kernel": "synth_frame_kernel (oscillator bank + filtered noise + their controls, fused)",
@@ -737,6 +769,10 @@ def main():
                                               "max_abs_diff": float((g - ref).abs().max())}
         result["scatter_gather"] = r
         del g, held
+        # the three N>1 rates side by side: left sharded (value), gathered on rank 0, and
+        # root-held controls scattered + audio gathered
+        result["value_gathered"] = result["gathered"]["value"]
+        result["value_scatter_gather"] = result["scatter_gather"]["value"]
 
     if rank == 0 and not args.no_op_leg:
         # op-boundary oscillator (core.py:136): per-sample inputs materialised in HBM
