@@ -117,6 +117,10 @@ __global__ void __launch_bounds__(256) controls_backward_kernel(
 // other workgroups' sine loops, as in the fused forward.
 constexpr int kKPT = 4;  // harmonics per thread
 
+// sine-loop placement padding per instantiation (tools/loop_align.py)
+template <int HMODE, int NOISE>
+constexpr bool kBwdLoopPad = true;
+
 template <int HMODE, int NOISE, bool RAW>
 __global__ void __launch_bounds__(512) frame_backward_kernel(
     const float* __restrict__ f0, const float* __restrict__ grad, const float* __restrict__ param,
@@ -231,9 +235,11 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
 #pragma unroll
         for (int c = 0; c < kKPT; ++c) acc2[c] = 0.0f;
         int j = j0;
-        // loop placement (tools/loop_align.py): one dword of padding puts this
-        // instantiation's 8-byte instructions at odd dword addresses, as the others already are
-        if constexpr (HMODE == 1 && NOISE == 0) asm volatile("s_nop 0");
+        // loop placement (tools/loop_align.py, pinned by tests/test_loop_align.py): the
+        // 8-byte instructions at odd dword addresses; the alignment point makes the placement
+        // independent of the code laid out before the loop, the s_nop flips it per instantiation
+        if constexpr (kBwdLoopPad<HMODE, NOISE>) asm volatile(".p2align 3\n s_nop 0");
+        else asm volatile(".p2align 3");
         for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
           const float2 p = wg[j], p1 = wg[j + 1];
           // the 8 chains written stage by stage so the scheduler keeps them interleaved (ILP 8)

@@ -106,13 +106,19 @@ constexpr float kLn10F = 2.30258512496948242188f;  // fl32(math.log(10)): ATen c
 constexpr float kOnePlusEps = 1.0f + 1e-4f;          // (True).float() + 1e-4  in fp32
 constexpr float kEps = 0.0f + 1e-4f;                 // (False).float() + 1e-4 in fp32
 
-// ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7.  sigmoid(x)**ln10 as
-// exp2(ln10 * log2(sigmoid)) on the hardware log/exp (relative error <~1e-6 for sigmoid >= 1e-3,
-// vs ~1 ulp for powf): 4% of the fused oscillator's time for a 1e-7-level amplitude change.
+// ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7, as
+//   sigmoid(x)**ln10 = exp2(-ln10 * log2(1 + 2^(-x log2 e)))
+// on the raw hardware v_exp_f32 / v_log_f32 (2^x and log2 x, ~1 ulp each, no range-reduction
+// wrappers): 3 transcendentals + 4 VALU ops, against ~60 VALU ops for the libm expf, IEEE
+// division, log2f and exp2f it replaced (the frame's controls run it H + NB + 1 times).  The
+// limits hold: x -> -inf gives 2^inf = inf, log2(inf) = inf, 2^-inf = 0 -> 1e-7; x -> +inf gives
+// log2(1) = 0 -> 2 + 1e-7.  Relative error against powf: ~ln2 ln10 |log2 sigmoid| ulp, i.e.
+// <~1e-6 at sigmoid >= 1e-3 (x >= -6.9) and 2e-6 at x = -12, the same order as the previous form.
 __device__ __forceinline__ float scale_fn(float x) {
-  const float sig = 1.0f / (1.0f + expf(-x));
-  const float p = exp2f(kLn10F * log2f(sig));
-  return 2.0f * p + 1e-7f;
+  constexpr float kLog2E = 1.44269502162933349609f;
+  const float e = __builtin_amdgcn_exp2f(x * -kLog2E);
+  const float l = __builtin_amdgcn_logf(1.0f + e);
+  return fmaf(2.0f, __builtin_amdgcn_exp2f(l * -kLn10F), 1e-7f);
 }
 
 // One harmonic-distribution entry of get_controls before normalisation (modules.py:53-60):
