@@ -313,6 +313,24 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
         if (d0 < d1) {
           float4 gc = *reinterpret_cast<const float4*>(gl + j0 + d0);
           int d = d0;
+          // 8 lags per iteration with the g window ping-ponged between two registers sets (no window
+          // moves) and a second accumulator set (8 independent FMA chains), summed at the end
+          float4 acc2 = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (; d + 8 <= d1; d += 8) {
+            const float4 xv = *reinterpret_cast<const float4*>(xl + d);
+            const float4 xw = *reinterpret_cast<const float4*>(xl + d + 4);
+            const float4 gn = *reinterpret_cast<const float4*>(gl + j0 + d + 4);
+            const float4 gm = *reinterpret_cast<const float4*>(gl + j0 + d + 8);
+            acc.x = fmaf(gc.x, xv.x, fmaf(gc.y, xv.y, fmaf(gc.z, xv.z, fmaf(gc.w, xv.w, acc.x))));
+            acc.y = fmaf(gc.y, xv.x, fmaf(gc.z, xv.y, fmaf(gc.w, xv.z, fmaf(gn.x, xv.w, acc.y))));
+            acc.z = fmaf(gc.z, xv.x, fmaf(gc.w, xv.y, fmaf(gn.x, xv.z, fmaf(gn.y, xv.w, acc.z))));
+            acc.w = fmaf(gc.w, xv.x, fmaf(gn.x, xv.y, fmaf(gn.y, xv.z, fmaf(gn.z, xv.w, acc.w))));
+            acc2.x = fmaf(gn.x, xw.x, fmaf(gn.y, xw.y, fmaf(gn.z, xw.z, fmaf(gn.w, xw.w, acc2.x))));
+            acc2.y = fmaf(gn.y, xw.x, fmaf(gn.z, xw.y, fmaf(gn.w, xw.z, fmaf(gm.x, xw.w, acc2.y))));
+            acc2.z = fmaf(gn.z, xw.x, fmaf(gn.w, xw.y, fmaf(gm.x, xw.z, fmaf(gm.y, xw.w, acc2.z))));
+            acc2.w = fmaf(gn.w, xw.x, fmaf(gm.x, xw.y, fmaf(gm.y, xw.z, fmaf(gm.z, xw.w, acc2.w))));
+            gc = gm;
+          }
           for (; d + 4 <= d1; d += 4) {
             const float4 xv = *reinterpret_cast<const float4*>(xl + d);
             const float4 gn = *reinterpret_cast<const float4*>(gl + j0 + d + 4);
@@ -322,6 +340,10 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
             acc.w = fmaf(gc.w, xv.x, fmaf(gn.x, xv.y, fmaf(gn.y, xv.z, fmaf(gn.z, xv.w, acc.w))));
             gc = gn;
           }
+          acc.x += acc2.x;
+          acc.y += acc2.y;
+          acc.z += acc2.z;
+          acc.w += acc2.w;
           for (; d < d1; ++d) {  // g is zero past bs, so taps c > 0 need no separate bound
             const float xv = xl[d];
             acc.x = fmaf(gl[j0 + d], xv, acc.x);

@@ -121,21 +121,30 @@ __device__ __forceinline__ bool frame_synth(
     coef[k] = make_float2((float)(k + 1), v);
   }
   if (n == 128 && NT >= 128) {
+    // irfft taps (core.py:150): ir[m] = (A0 + (-1)^m A64 + 2 (O(m) + E(m))) / 128 with O the odd-k and E
+    // the even-k (2..62) cosine sums.  Since cos(2 pi k (64 - m) / 128) = (-1)^k cos(2 pi k m / 128),
+    // ir[64 - m] = (A0 + (-1)^m A64 + 2 (E(m) - O(m))) / 128: lane 2m + p of the first wave sums one
+    // parity (32 terms, k ascending as before) for m in [0, 32) and the lane pair exchanges its sums by
+    // DPP, so the wave issues 32 multiply-adds instead of 63 for all 64 taps; the second wave sums
+    // ir[32] across its lanes
     if (tid < 64) {
-      const int m = tid;
-      float s0 = 0.0f, s1 = 0.0f;
+      const int m = tid >> 1, p = tid & 1;
+      float sum = 0.0f;
 #pragma unroll 8
-      for (int k = 1; k < 63; k += 2) {
-        s0 = fmaf(A[k], kIrCos128[k * 64 + m], s0);
-        s1 = fmaf(A[k + 1], kIrCos128[(k + 1) * 64 + m], s1);
+      for (int j = 0; j < 32; ++j) {
+        const int k = 2 * j + p;  // even lanes: k = 0 (a zero term), 2, ..., 62; odd lanes: 1, ..., 63
+        sum = fmaf(k ? A[k] : 0.0f, kIrCos128[k * 64 + m], sum);
       }
-      s0 = fmaf(A[63], kIrCos128[63 * 64 + m], s0);
-      ir[m] = (A[0] + ((m & 1) ? -A[64] : A[64]) + 2.0f * (s0 + s1)) * (1.0f / 128.0f);
-    } else if (tid < 128) {  // tap n/2: cos(pi k) = (-1)^k
-      float alt = (tid - 64 >= 1 && tid - 64 < 64) ? (((tid - 64) & 1) ? -A[tid - 64] : A[tid - 64]) : 0.0f;
+      const float other = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xB1, 0xF, 0xF, true));
+      const float a0 = A[0] + ((m & 1) ? -A[64] : A[64]);
+      if (p == 0) ir[m] = (a0 + 2.0f * (other + sum)) * (1.0f / 128.0f);       // odd + even
+      else ir[64 - m] = (a0 + 2.0f * (other - sum)) * (1.0f / 128.0f);        // even - odd
+    } else if (tid < 128) {  // tap n/2 = 32: A0 + A64 + 2 sum_k A_k cos(pi k / 2)
+      const int k = tid - 64;
+      float t = k >= 1 ? A[k] * kIrCos128[k * 64 + 32] : 0.0f;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
-      if (tid == 64) ir[64] = (A[0] + A[64] + 2.0f * alt) * (1.0f / 128.0f);
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (tid == 64) ir[32] = (A[0] + A[64] + 2.0f * t) * (1.0f / 128.0f);
     }
   } else {
     for (int m = tid; m <= half; m += NT) ir[m] = irfft_tap(A, ct, n, m);
@@ -153,16 +162,40 @@ __device__ __forceinline__ bool frame_synth(
   __syncthreads();
 
   // ---- phase 4: noise tail (taps past bs - n/2 reach only the last n/2 outputs) ----
-  // with n/2 = 64 (65 bands) and h zero for the 63 positions below tail_start (written in phase 3) every
-  // lane runs the same 64 taps, unrolled with no per-tap predication: the taps past l add fma(0, x, c) = c,
-  // the others come in tap order, so the sums are the loop's below (measured 1.2 % faster)
+  // With n/2 = 64 (65 bands) and h zero for the 63 positions below tail_start (written in phase 3), the
+  // 64 x 64 tap triangle runs unpredicated (the taps past l add fma(0, x, c) = c) and register-blocked on
+  // the first wave: lane 4g + q computes outputs 4g..4g+3 over the taps d in [16q, 16q + 16) from 4 + 5
+  // ds_read_b128 (x[16q..], h[tail_start + 4g - 16q - 16 ..]), then the four tap quarters are summed across
+  // the lane quad by DPP (quad_perm): ~90 wave-instructions instead of 64 x 3 for one output per lane.
   if (bs - tail_start == 64 && bs - 127 >= lo_end) {
-    for (int l = tid; l < 64; l += NT) {
-      const float* hj = h + tail_start + l;
-      float c = 0.0f;
-#pragma unroll 16
-      for (int d = 0; d < 64; ++d) c = fmaf(hj[-d], x[d], c);
-      tail[l] = c;
+    if (tid < 64) {
+      const int g = tid >> 2, q = tid & 3;
+      const float4* x4 = reinterpret_cast<const float4*>(x) + 4 * q;
+      const float4* h4 = reinterpret_cast<const float4*>(h + tail_start + 4 * g - 16 * q - 16);
+      float xv[16], hv[20];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 v = x4[i];
+        xv[4 * i] = v.x; xv[4 * i + 1] = v.y; xv[4 * i + 2] = v.z; xv[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const float4 v = h4[i];
+        hv[4 * i] = v.x; hv[4 * i + 1] = v.y; hv[4 * i + 2] = v.z; hv[4 * i + 3] = v.w;
+      }
+      float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      // output l = 4g + r, tap d = 16q + dd: h[tail_start + l - d] = hv[16 + r - dd] (hv[0] unused)
+#pragma unroll
+      for (int dd = 0; dd < 16; ++dd) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = fmaf(hv[16 + r - dd], xv[dd], c[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        c[r] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(c[r]), 0xB1, 0xF, 0xF, true));  // q ^ 1
+        c[r] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(c[r]), 0x4E, 0xF, 0xF, true));  // q ^ 2
+      }
+      if (q == 0) *reinterpret_cast<float4*>(tail + 4 * g) = make_float4(c[0], c[1], c[2], c[3]);
     }
   } else
   for (int l = tid; l < bs - tail_start; l += NT) {
