@@ -107,18 +107,29 @@ constexpr float kOnePlusEps = 1.0f + 1e-4f;          // (True).float() + 1e-4  i
 constexpr float kEps = 0.0f + 1e-4f;                 // (False).float() + 1e-4 in fp32
 
 // ddsp/core.py:77-78  scale_function: 2 * sigmoid(x) ** ln(10) + 1e-7, as
-//   sigmoid(x)**ln10 = exp2(-ln10 * log2(1 + 2^(-x log2 e)))
-// on the raw hardware v_exp_f32 / v_log_f32 (2^x and log2 x, ~1 ulp each, no range-reduction
-// wrappers): 3 transcendentals + 4 VALU ops, against ~60 VALU ops for the libm expf, IEEE
-// division, log2f and exp2f it replaced (the frame's controls run it H + NB + 1 times).  The
-// limits hold: x -> -inf gives 2^inf = inf, log2(inf) = inf, 2^-inf = 0 -> 1e-7; x -> +inf gives
-// log2(1) = 0 -> 2 + 1e-7.  Relative error against powf: ~ln2 ln10 |log2 sigmoid| ulp, i.e.
-// <~1e-6 at sigmoid >= 1e-3 (x >= -6.9) and 2e-6 at x = -12, the same order as the previous form.
+//   sigmoid(x)**ln10 = 2^(-ln10 * l),  l = log2(1 + 2^a),  a = -x log2(e)
+// on the raw hardware v_exp_f32 / v_log_f32 (2^x, log2 x; 3 transcendentals, ~20 VALU ops against
+// ~60 for the libm expf, IEEE division, log2f and exp2f of the first form).  l is carried as a
+// double-float: l = max(a, 0) + log2(1 + 2^-|a|) with a's rounding error (an fma) kept beside it, so
+// the large exponents of small sigmoids (l ~ 17 at x = -12) lose no bits, and the final 2^b takes the
+// low part as 2^b_hi (1 + b_lo ln2).  Relative error ~3e-7 over x in [-25, 12] with 0.5-ulp
+// transcendentals (numpy emulation against fp64), ~5x below the first form's.  x < -100 is clamped
+// (the result is 1e-7 there either way; keeps -inf from making a NaN; NaN stays NaN).
 __device__ __forceinline__ float scale_fn(float x) {
-  constexpr float kLog2E = 1.44269502162933349609f;
-  const float e = __builtin_amdgcn_exp2f(x * -kLog2E);
-  const float l = __builtin_amdgcn_logf(1.0f + e);
-  return fmaf(2.0f, __builtin_amdgcn_exp2f(l * -kLn10F), 1e-7f);
+  constexpr float kLog2E = 1.44269502162933349609f;          // fl32(log2 e)
+  constexpr float kLog2ELo = 1.92596298909109e-08f;          // log2 e - kLog2E
+  constexpr float kLn2 = 0.693147180559945309f;
+  const float xc = x < -100.0f ? -100.0f : x;
+  const float a = xc * -kLog2E;
+  const float a_lo = fmaf(-xc, kLog2E, -a) + (-xc) * kLog2ELo;   // a + a_lo = -x log2(e)
+  const float m = fmaxf(a, 0.0f);
+  const float t = __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(-fabsf(a)));
+  const float lh = m + t;
+  const float ll = (a > 0.0f ? a_lo : 0.0f) + ((m - lh) + t);
+  const float bh = lh * -kLn10F;
+  const float bl = fmaf(lh, -kLn10F, -bh) + ll * -kLn10F;
+  const float pe = __builtin_amdgcn_exp2f(bh);
+  return fmaf(2.0f, fmaf(pe, bl * kLn2, pe), 1e-7f);
 }
 
 // One harmonic-distribution entry of get_controls before normalisation (modules.py:53-60):
