@@ -16,6 +16,10 @@ tail -1 gpurun_out/pytest_$TAG.log
 step smoke
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { cat gpurun_out/smoke_$TAG.log; exit 1; }
 tail -1 gpurun_out/smoke_$TAG.log
+step bench-driver-command
+# the driver's exact command (BENCH_rNN.json): 20 timed steps after 5 warmup steps
+timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_driver.json \
+  2> gpurun_out/bench_${TAG}_driver.err || { tail -20 gpurun_out/bench_${TAG}_driver.err; exit 1; }
 step bench
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 step bench-config4
