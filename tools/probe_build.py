@@ -1,0 +1,56 @@
+"""Phase-removal probe builds of the fused synthesis kernel (measurement only, never shipped):
+a copy of csrc/synth_frame.hip with one phase edited out is compiled into build/ab_<name>.so
+(linked with the in-tree objects), so PMC passes (tools/pmc_probe.sh through DDSP_HIP_LIB) give
+each phase's dynamic VALU count by difference.  Outputs of these builds are wrong by design.
+
+    python tools/probe_build.py [name ...]      (default: every probe below)
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc", "synth_frame.hip")
+
+# name -> [(literal, replacement)]; every literal must occur in the source
+PROBES = {
+    "noprefix": [("for (int g = tid; g < f; g += NT)", "for (int g = tid; g < 0; g += NT)")],
+    "noscale": [("const float sv = scale_fn(i >= H && i < H + NB ? raw + bias : raw);",
+                 "const float sv = raw;")],
+    "norng": [("const Philox4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), off0, off1, k0, k1);",
+               "Philox4 r; r.v[0] = (uint32_t)q; r.v[1] = off0; r.v[2] = k0; r.v[3] = (uint32_t)t;")],
+    "noirfft": [("if (n == 128 && NT >= 128) {", "if (n == 128 && NT >= 128) { if (tid <= 64) ir[tid] = A[tid]; } else if (false) {")],
+    "notail": [("if (bs - tail_start == 64 && bs - 127 >= lo_end) {\n    if (tid < 64) {",
+                "if (bs - tail_start == 64 && bs - 127 >= lo_end) {\n    if (tid < 0) {")],
+    "nohtaps": [("h[j] = ir_at_half(ir, ct, n, bs, j);", "h[j] = ir[j & 63];")],
+    "noosc": [("osc_bank4(coef, H4, w, acc);", "acc[0] = w[0]; acc[1] = w[1]; acc[2] = w[2]; acc[3] = w[3];")],
+    "nofir": [("float4 y = fir4(h, x, j0, lo_end, bs, bs);", "float4 y = make_float4(x[j0], x[j0 + 1], h[j0], h[j0 + 3]);")],
+}
+
+
+def build(name):
+    src = open(SRC).read()
+    for a, b in PROBES[name]:
+        if a not in src:
+            raise SystemExit(f"probe {name}: pattern not found: {a[:60]}")
+        src = src.replace(a, b)
+    d = os.path.join(ROOT, "build", f"probe_{name}")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, "synth_frame.hip")
+    open(path, "w").write(src)
+    inc = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc")
+    obj = os.path.join(ROOT, "build", f"ab_{name}_synth_frame.o")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                    "-ffp-contract=off", f"-I{ROOT}/include", f"-I{ROOT}/build", f"-I{inc}",
+                    "-Wno-unused-result", "-fno-slp-vectorize", "-c", path, "-o", obj], check=True)
+    objs = [os.path.join(ROOT, "build", f) for f in sorted(os.listdir(os.path.join(ROOT, "build")))
+            if f.endswith(".o") and not f.startswith("ab_") and f != "synth_frame.o"]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o",
+                    os.path.join(ROOT, "build", f"ab_{name}.so")] + objs + [obj], check=True)
+    print("built", f"build/ab_{name}.so", flush=True)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(PROBES):
+        build(n)
