@@ -129,12 +129,14 @@ __device__ __forceinline__ bool frame_synth(
     // ir[32] across its lanes
     if (tid < 64) {
       const int m = tid >> 1, p = tid & 1;
-      float sum = 0.0f;
-#pragma unroll 8
-      for (int j = 0; j < 32; ++j) {
-        const int k = 2 * j + p;  // even lanes: k = 0 (a zero term), 2, ..., 62; odd lanes: 1, ..., 63
-        sum = fmaf(k ? A[k] : 0.0f, kIrCos128[k * 64 + m], sum);
-      }
+      // k = 2j + p: even lanes k = 0 (a zero term), 2, ..., 62; odd lanes 1, ..., 63.  One base per
+      // lane and fully unrolled constant offsets (128 floats per j in the table, 2 in A): a load and
+      // an FMA per term, no per-term address arithmetic (the PMC probe counted ~5 VALU per term)
+      const float* cm = kIrCos128 + p * 64 + m;
+      const float* ap = A + p;
+      float sum = fmaf(p ? ap[0] : 0.0f, cm[0], 0.0f);
+#pragma unroll
+      for (int j = 1; j < 32; ++j) sum = fmaf(ap[2 * j], cm[128 * j], sum);
       const float other = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xB1, 0xF, 0xF, true));
       const float a0 = A[0] + ((m & 1) ? -A[64] : A[64]);
       if (p == 0) ir[m] = (a0 + 2.0f * (other + sum)) * (1.0f / 128.0f);       // odd + even
