@@ -542,6 +542,35 @@ def gru(x, gru_module, h0=None):
     return out, h_last
 
 
+def layer_norm_leaky_relu(h, norm, act, out=None, w1=None, b1=None):
+    """ddsp/core.py:122-129 after one block's Linear: LeakyReLU(LayerNorm(h)) in one pass
+    (ddsp_hip_layer_norm_leaky_relu).  h [..., cols] contiguous; or, with w1/b1 (a Linear with one input
+    feature), h [..., 1] is that Linear's input and the block's pre-activation is h * w1 + b1.  ``out``
+    (optional) may be a column slice of a wider buffer with one row stride.  Returns None where the
+    kernel does not apply (the caller runs torch's modules); inference only."""
+    _dev(h, norm.weight, norm.bias)
+    cols = int(norm.normalized_shape[-1])
+    if len(norm.normalized_shape) != 1 or (w1 is None and h.shape[-1] != cols) or (w1 is not None and h.shape[-1] != 1):
+        return None
+    if not h.is_contiguous():
+        h = h.contiguous()
+    lead = tuple(h.shape[:-1])
+    rows = h.numel() // h.shape[-1] if h.shape[-1] else 0
+    if out is None:
+        out = torch.empty(*lead, cols, dtype=torch.float32, device=h.device)
+    elif (tuple(out.shape) != lead + (cols,) or out.stride(-1) != 1 or
+          any(out.stride(i) != out.stride(i + 1) * out.shape[i + 1] for i in range(out.dim() - 2))):
+        return None
+    y_ld = out.stride(-2) if out.dim() >= 2 else cols
+    g, b = _c(norm.weight), _c(norm.bias)
+    w1c = _c(w1) if w1 is not None else None
+    b1c = _c(b1) if b1 is not None else None
+    st = _lib.call("layer_norm_leaky_relu", _lib.ptr(h), int(h.shape[-1]), _lib.ptr(w1c), _lib.ptr(b1c), _lib.ptr(g),
+                   _lib.ptr(b), float(norm.eps), float(act.negative_slope), _lib.ptr(out), int(y_ld), int(rows), cols,
+                   _lib.stream_of(out), allow=(ERANGE,))
+    return None if st == ERANGE else out
+
+
 def dense_input(x, width=None, ld=None, scale=1.0, shift=0.0, first=None, norm=None, x_copy=None):
     """One input segment of dense_rows: x [rows, ld] (or, with `first` = a K=1 nn.Linear, one value
     per row at x[r * ld]); `norm` = an nn.LayerNorm applied with LeakyReLU(0.01) after it."""

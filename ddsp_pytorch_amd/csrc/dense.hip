@@ -182,6 +182,63 @@ __global__ void __launch_bounds__(kDenseNT) dense_rows_kernel(DenseArgs args) {
 
 using namespace ddsp;
 
+// ---------------------------------------------------------------------------------------------
+// The decoder's MLP blocks at full batch (ddsp/core.py:122-129: Linear -> LayerNorm -> LeakyReLU):
+// the Linear stays a hipBLASLt GEMM, and LayerNorm + LeakyReLU run as ONE pass over its output
+// (torch runs two: 18 + 11 us per [12800, 512] layer at config 2), one wave per row, the row in
+// registers (cols/64 values per lane), mean and biased variance by two wave sums (two-pass, as
+// accurate as torch's Welford), eps inside the root as torch does.  With w1/b1 the block's Linear
+// has one input feature (the f0 / loudness MLPs' first layer, decoder.py:25-30): h = x w1 + b1 is
+// formed on the fly (product, then bias: the GEMM's two roundings).  y may be a column slice of a
+// wider buffer (y_ld), so the f0 and loudness MLPs write straight into the GRU's input
+// concatenation (decoder.py:46-49) with no torch.cat.
+template <int V4>  // float4 per lane: cols = 256 * V4
+__global__ void __launch_bounds__(256) ln_leaky_kernel(const float* __restrict__ x, int64_t x_ld,
+                                                       const float* __restrict__ w1, const float* __restrict__ b1,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, float slope, float* __restrict__ y, int64_t y_ld,
+                                                       int64_t rows) {
+  constexpr int C = 256 * V4;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  float4 v[V4];
+  if (w1) {
+    const float xv = x[row * x_ld];
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      const float4 w = reinterpret_cast<const float4*>(w1)[lane + 64 * i];
+      const float4 b = reinterpret_cast<const float4*>(b1)[lane + 64 * i];
+      v[i] = make_float4(xv * w.x + b.x, xv * w.y + b.y, xv * w.z + b.z, xv * w.w + b.w);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V4; ++i) v[i] = reinterpret_cast<const float4*>(x + row * x_ld)[lane + 64 * i];
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) * (1.0f / (float)C);
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q += (a * a + b * b) + (c * c + d * d);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / (float)C) + eps);
+  float4* yr = reinterpret_cast<float4*>(y + row * y_ld);
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    const float4 g = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
+    const float4 bt = reinterpret_cast<const float4*>(beta)[lane + 64 * i];
+    float o[4] = {(v[i].x - mean) * rstd * g.x + bt.x, (v[i].y - mean) * rstd * g.y + bt.y,
+                  (v[i].z - mean) * rstd * g.z + bt.z, (v[i].w - mean) * rstd * g.w + bt.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = o[e] >= 0.0f ? o[e] : o[e] * slope;
+    yr[lane + 64 * i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 extern "C" {
 
 int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream) {
@@ -212,6 +269,26 @@ int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, 
   if (max_k > 64 * kKL || max_n > (int64_t)65535 * kOutPerWG) return DDSP_HIP_ERANGE;
   const dim3 grid((unsigned)((max_n + kOutPerWG - 1) / kOutPerWG), (unsigned)n_problems);
   hipLaunchKernelGGL(dense_rows_kernel, grid, dim3(kDenseNT), shm, reinterpret_cast<hipStream_t>(stream), args);
+  return launch_status();
+}
+
+int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1, const float* b1, const float* gamma,
+                                   const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
+                                   int64_t cols, void* stream) {
+  if (rows < 0 || cols < 1 || !gamma || !beta || (!w1) != (!b1)) return DDSP_HIP_EINVAL;
+  if (rows == 0) return DDSP_HIP_OK;
+  if (!x || !y || y_ld < cols || (!w1 && x_ld < cols) || (w1 && x_ld < 1)) return DDSP_HIP_EINVAL;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(gamma) |
+                       reinterpret_cast<uintptr_t>(beta) | (w1 ? reinterpret_cast<uintptr_t>(w1) |
+                       reinterpret_cast<uintptr_t>(b1) : reinterpret_cast<uintptr_t>(x));
+  if ((cols != 512 && cols != 1024) || (al & 15) || (y_ld & 3) || (!w1 && (x_ld & 3)) || rows > (int64_t)4 * 0x7fffffff)
+    return DDSP_HIP_ERANGE;  // callers keep torch's LayerNorm + LeakyReLU
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (cols == 512)
+    hipLaunchKernelGGL(ln_leaky_kernel<2>, grid, dim3(256), 0, st, x, x_ld, w1, b1, gamma, beta, eps, slope, y, y_ld, rows);
+  else
+    hipLaunchKernelGGL(ln_leaky_kernel<4>, grid, dim3(256), 0, st, x, x_ld, w1, b1, gamma, beta, eps, slope, y, y_ld, rows);
   return launch_status();
 }
 

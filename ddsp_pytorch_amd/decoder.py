@@ -51,19 +51,82 @@ def _gru(mod, hidden, h0):
     return mod.gru(hidden, h0) if h0 is not None else mod.gru(hidden)
 
 
+def _mlp_fusable(seq, x):
+    """An unobserved (Linear, LayerNorm, LeakyReLU) x n block chain (ddsp/core.py:122-129) on the GPU at
+    inference: the LayerNorm + LeakyReLU pairs may run as one kernel."""
+    from torch.nn.modules import module as _m
+    if not x.is_cuda or torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in seq.parameters())):
+        return False
+    if _m._global_forward_hooks or _m._global_forward_pre_hooks or seq._forward_hooks or seq._forward_pre_hooks:
+        return False
+    if type(seq) is not nn.Sequential or type(seq).forward is not nn.Sequential.forward:
+        return False
+    mods = list(seq)
+    if len(mods) % 3:
+        return False
+    for i in range(0, len(mods), 3):
+        lin, ln, act = mods[i:i + 3]
+        if (type(lin) is not nn.Linear or type(ln) is not nn.LayerNorm or type(act) is not nn.LeakyReLU or
+                lin.bias is None or not ln.elementwise_affine or ln.bias is None or
+                any(m._forward_hooks or m._forward_pre_hooks for m in (lin, ln, act))):
+            return False
+    return True
+
+
+def mlp_forward(seq, x, out=None):
+    """seq(x) for a core.py:122-129 MLP; on the GPU at inference each block's LayerNorm + LeakyReLU is one
+    kernel (core.layer_norm_leaky_relu) after the Linear's GEMM, a one-feature first Linear folds into it,
+    and the last block may write into ``out`` (e.g. a column slice of the GRU input concatenation)."""
+    if not _mlp_fusable(seq, x):
+        y = seq(x)
+        if out is None:
+            return y
+        out.copy_(y)
+        return out
+    mods = list(seq)
+    h = x
+    for i in range(0, len(mods), 3):
+        lin, ln, act = mods[i:i + 3]
+        dst = out if i + 3 == len(mods) else None
+        if lin.in_features == 1:
+            y = core.layer_norm_leaky_relu(h, ln, act, out=dst, w1=lin.weight[:, 0], b1=lin.bias)
+            if y is None:
+                y = act(ln(lin(h)))
+        else:
+            g = torch.nn.functional.linear(h, lin.weight, lin.bias)
+            y = core.layer_norm_leaky_relu(g, ln, act, out=dst)
+            if y is None:
+                y = act(ln(g))
+        if dst is not None and y is not dst:
+            dst.copy_(y)
+            y = dst
+        h = y
+    return h
+
+
 def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
     """ddsp/models/decoder.py:43-68 GRUDecoder.forward (incl. the optional z projection), the GRU on
-    the step kernel for inference.  install() binds it to the reference's GRUDecoder too."""
-    hidden = torch.cat([self.f0_mlp(f0), self.loudness_mlp(loudness)], -1)
+    the step kernel for inference.  install() binds it to the reference's GRUDecoder too.  At inference
+    on the GPU the MLP blocks' LayerNorm + LeakyReLU run fused and the input MLPs write straight into
+    the GRU's input concatenation (mlp_forward)."""
+    mlps = [(self.f0_mlp, f0), (self.loudness_mlp, loudness)]
     if getattr(self, "add_z", False):
         assert z is not None
-        hidden = torch.cat([hidden, self.z_mlp(z)], -1)
+        mlps.append((self.z_mlp, z))
+    widths = [m[-3].out_features if len(m) >= 3 else -1 for m, _ in mlps]
+    if all(_mlp_fusable(m, x) for m, x in mlps) and len(set(widths)) == 1:
+        W = widths[0]
+        hidden = torch.empty(*f0.shape[:-1], W * len(mlps), dtype=torch.float32, device=f0.device)
+        for i, (m, x) in enumerate(mlps):
+            mlp_forward(m, x, out=hidden[..., i * W:(i + 1) * W])
+    else:
+        hidden = torch.cat([m(x) for m, x in mlps], -1)
     if realtime:
         gru_out, cache = _gru(self, hidden, self.cache_gru)
         self.cache_gru.copy_(cache)
     else:
         gru_out = _gru(self, hidden, None)[0]
-    return self.out_mlp(torch.cat([gru_out, f0, loudness], -1))
+    return mlp_forward(self.out_mlp, torch.cat([gru_out, f0, loudness], -1))
 
 
 def _hooked(m):

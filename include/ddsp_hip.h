@@ -224,6 +224,15 @@ typedef struct ddsp_hip_dense_problem {
 } ddsp_hip_dense_problem;
 int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream);
 
+/* ddsp/core.py:122-129 (one MLP block after its Linear, decoder.py:25-42): y = LeakyReLU(LayerNorm(h))
+ * per row of cols features, h = x [rows, x_ld] or, with w1/b1 (a Linear with ONE input feature),
+ * h = x[r] * w1 + b1 formed on the fly.  gamma/beta: the LayerNorm's affine; eps and the negative
+ * slope as in torch (1e-5, 0.01).  y [rows, y_ld] may be a column slice of a wider buffer.  One pass
+ * instead of torch's two; cols 512 or 1024 with 16-byte aligned rows, else DDSP_HIP_ERANGE. */
+int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1, const float* b1, const float* gamma,
+                                   const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
+                                   int64_t cols, void* stream);
+
 /* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
  * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,
  * computed by the caller's GEMM), W_hh[3H,H], b_hh[3H] in torch's (r, z, n) order; h0 [B,H]

@@ -1,0 +1,60 @@
+"""The decoder's MLP blocks (ddsp/core.py:122-129) with LayerNorm + LeakyReLU fused into one kernel
+(core.layer_norm_leaky_relu, decoder.mlp_forward) against torch's modules on the same device, incl.
+the one-feature first Linear folded into the kernel and outputs written into a column slice."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dd():
+    import ddsp_pytorch_amd
+    return ddsp_pytorch_amd
+
+
+@pytest.mark.parametrize("in_size,hidden", [(1, 512), (514, 512), (512, 1024), (1, 1024)])
+def test_mlp_forward_matches_torch(dd, in_size, hidden):
+    from ddsp_pytorch_amd.decoder import mlp, mlp_forward
+    torch.manual_seed(0)
+    m = mlp(in_size, hidden, 3).cuda().eval()
+    with torch.no_grad():  # non-trivial affine parameters
+        for mod in m:
+            if isinstance(mod, torch.nn.LayerNorm):
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(7, 33, in_size, device="cuda") * 3.0
+    with torch.no_grad():
+        ref = m(x)
+        got = mlp_forward(m, x)
+        wide = torch.full((7, 33, 3 * hidden), 7.0, device="cuda")
+        into = mlp_forward(m, x, out=wide[..., hidden:2 * hidden])
+    torch.testing.assert_close(got, ref, rtol=2e-5, atol=2e-5)
+    assert into.data_ptr() == wide[..., hidden:].data_ptr()
+    torch.testing.assert_close(wide[..., hidden:2 * hidden], ref, rtol=2e-5, atol=2e-5)
+    assert torch.all(wide[..., :hidden] == 7.0) and torch.all(wide[..., 2 * hidden:] == 7.0)
+
+
+def test_layer_norm_leaky_relu_kernel(dd):
+    torch.manual_seed(1)
+    ln = torch.nn.LayerNorm(512).cuda()
+    act = torch.nn.LeakyReLU()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+        h = torch.randn(1001, 512, device="cuda") * 10 + 3
+        y = dd.core.layer_norm_leaky_relu(h, ln, act)
+        torch.testing.assert_close(y, act(ln(h)), rtol=1e-5, atol=1e-5)
+        # outside the kernel's shapes: None (the caller keeps torch's modules)
+        assert dd.core.layer_norm_leaky_relu(torch.randn(4, 100, device="cuda"), torch.nn.LayerNorm(100).cuda(),
+                                             act) is None
+
+
+def test_mlp_under_autograd_keeps_torch(dd):
+    """Training keeps torch's modules (their autograd): the fused path is inference-only."""
+    from ddsp_pytorch_amd.decoder import _mlp_fusable, mlp
+    m = mlp(1, 512, 3).cuda()
+    x = torch.randn(2, 5, 1, device="cuda")
+    assert not _mlp_fusable(m, x)
+    with torch.no_grad():
+        assert _mlp_fusable(m, x)
