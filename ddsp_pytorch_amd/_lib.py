@@ -117,7 +117,10 @@ def load():
                     f"ddsp_hip: native library not found at {LIB_PATH}; run `make` "
                     "(or __graft_entry__.build()) — there is no CPU fallback")
             lib = ctypes.CDLL(LIB_PATH)
+            variant = "DDSP_HIP_LIB" in os.environ  # an A/B build of another revision (tools/ab_*.sh)
             for name, (res, args) in SIGNATURES.items():
+                if variant and not hasattr(lib, name):
+                    continue  # an entry point that revision does not have: absent, not an error
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args

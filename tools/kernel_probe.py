@@ -1,6 +1,6 @@
 """Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
 
-    python tools/kernel_probe.py {fused,bwd,reverb_bwd,harmonic,harmonic_frames,noise,reverb,op} [reps]
+    python tools/kernel_probe.py {fused,bwd,reverb_bwd,gru,harmonic,harmonic_frames,noise,reverb,op} [reps]
 """
 import os
 import sys
@@ -26,6 +26,15 @@ def main():
         g = torch.randn_like(out)
         for _ in range(reps):
             out.backward(g, retain_graph=True)
+        torch.cuda.synchronize()
+        return
+    if which == "gru":  # the decoder's GRU recurrence (B=64, T=200, hidden 512): step kernels
+        torch.manual_seed(0)
+        g = torch.nn.GRU(1024, 512, batch_first=True).to(dev)
+        xg = torch.randn(B, F, 1024, device=dev)
+        with torch.no_grad():
+            for _ in range(reps):
+                core.gru(xg, g)
         torch.cuda.synchronize()
         return
     if which == "reverb_bwd":  # the UPOLS backward (input and IR gradients)

@@ -1,7 +1,8 @@
-"""Phase-removal probe builds of the fused synthesis kernel (measurement only, never shipped):
-a copy of csrc/synth_frame.hip with one phase edited out is compiled into build/ab_<name>.so
-(linked with the in-tree objects), so PMC passes (tools/pmc_probe.sh through DDSP_HIP_LIB) give
-each phase's dynamic VALU count by difference.  Outputs of these builds are wrong by design.
+"""Probe / variant builds (measurement only, never shipped): a copy of one csrc/<stem>.hip with
+literal edits is compiled into build/ab_<name>.so (linked with the in-tree objects).  The synth_frame
+probes edit one phase out, so PMC passes (tools/pmc_variants.sh through DDSP_HIP_LIB) give each
+phase's dynamic VALU count by difference — their outputs are wrong by design; the gru_* variants
+change the step kernel's tile shape (outputs equal up to summation order).
 
     python tools/probe_build.py [name ...]      (default: every probe below)
 """
@@ -11,10 +12,13 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc", "synth_frame.hip")
+CSRC = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc")
 
 # name -> [(literal, replacement)]; every literal must occur in the source
+STEM = {"gru16": "gru", "gru64": "gru"}
 PROBES = {
+    "gru16": [("constexpr int kBS = 32;", "constexpr int kBS = 16;"), ("constexpr int kKC = 16;", "constexpr int kKC = 32;")],
+    "gru64": [("constexpr int kBS = 32;", "constexpr int kBS = 64;"), ("constexpr int kKC = 16;", "constexpr int kKC = 8;")],
     "noprefix": [("for (int g = tid; g < f; g += NT)", "for (int g = tid; g < 0; g += NT)")],
     "noscale": [("const float sv = scale_fn(i >= H && i < H + NB ? raw + bias : raw);",
                  "const float sv = raw;")],
@@ -30,22 +34,23 @@ PROBES = {
 
 
 def build(name):
-    src = open(SRC).read()
+    stem = STEM.get(name, "synth_frame")
+    src = open(os.path.join(CSRC, stem + ".hip")).read()
     for a, b in PROBES[name]:
         if a not in src:
             raise SystemExit(f"probe {name}: pattern not found: {a[:60]}")
         src = src.replace(a, b)
     d = os.path.join(ROOT, "build", f"probe_{name}")
     os.makedirs(d, exist_ok=True)
-    path = os.path.join(d, "synth_frame.hip")
+    path = os.path.join(d, stem + ".hip")
     open(path, "w").write(src)
     inc = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc")
-    obj = os.path.join(ROOT, "build", f"ab_{name}_synth_frame.o")
+    obj = os.path.join(ROOT, "build", f"ab_{name}_{stem}.o")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                     "-ffp-contract=off", f"-I{ROOT}/include", f"-I{ROOT}/build", f"-I{inc}",
                     "-Wno-unused-result", "-fno-slp-vectorize", "-c", path, "-o", obj], check=True)
     objs = [os.path.join(ROOT, "build", f) for f in sorted(os.listdir(os.path.join(ROOT, "build")))
-            if f.endswith(".o") and not f.startswith("ab_") and f != "synth_frame.o"]
+            if f.endswith(".o") and not f.startswith("ab_") and f != stem + ".o"]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o",
                     os.path.join(ROOT, "build", f"ab_{name}.so")] + objs + [obj], check=True)
     print("built", f"build/ab_{name}.so", flush=True)
