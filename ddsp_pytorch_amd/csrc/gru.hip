@@ -6,8 +6,8 @@
 //   n = tanh(xp_n + r * (W_hn h + b_hn)),  h' = (1 - z) * n + z * h
 // where xp = x W_ih^T + b_ih for every time step at once is one plain GEMM (the caller's
 // hipBLASLt matmul).  The recurrence is what MIOpen spends ~45 us per step on at batch 64,
-// hidden 512: here one launch per step, 256 workgroups (hidden slices of 4 units x batch tiles
-// of 32), each holding its 12 rows of W_hh in LDS and its batch tile's h chunk in registers;
+// hidden 512: here one launch per step, 512 workgroups (hidden slices of 4 units x batch tiles
+// of 16), each holding its 12 rows of W_hh in LDS and its batch tile's h chunk in registers;
 // the kernel boundary is the step's grid-wide barrier (no persistent spin, no residency
 // requirement).  h_t is written straight into the output sequence, which is the next step's h.
 #include <hip/hip_runtime.h>
@@ -20,8 +20,8 @@ namespace ddsp {
 namespace {
 
 constexpr int kHS = 4;    // hidden units per workgroup
-constexpr int kBS = 32;   // batch rows per workgroup
-constexpr int kKC = 16;   // k-chunks (threads per batch row)
+constexpr int kBS = 16;   // batch rows per workgroup (16: 7.7-7.9 us per step at config 2; 32: 8.4-8.5, 64: 11.9)
+constexpr int kKC = 32;   // k-chunks (threads per batch row)
 constexpr int kNT = kBS * kKC;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }

@@ -15,10 +15,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc")
 
 # name -> [(literal, replacement)]; every literal must occur in the source
-STEM = {"gru16": "gru", "gru64": "gru"}
+STEM = {"gru8": "gru", "gru16h2": "gru", "gru16h8": "gru", "gru32": "gru"}
 PROBES = {
-    "gru16": [("constexpr int kBS = 32;", "constexpr int kBS = 16;"), ("constexpr int kKC = 16;", "constexpr int kKC = 32;")],
-    "gru64": [("constexpr int kBS = 32;", "constexpr int kBS = 64;"), ("constexpr int kKC = 16;", "constexpr int kKC = 8;")],
+    "gru8": [("constexpr int kBS = 16;", "constexpr int kBS = 8;"), ("constexpr int kKC = 32;", "constexpr int kKC = 64;")],
+    "gru32": [("constexpr int kBS = 16;", "constexpr int kBS = 32;"), ("constexpr int kKC = 32;", "constexpr int kKC = 16;")],
+    "gru16h2": [("constexpr int kHS = 4;", "constexpr int kHS = 2;")],
+    "gru16h8": [("constexpr int kHS = 4;", "constexpr int kHS = 8;")],
     "noprefix": [("for (int g = tid; g < f; g += NT)", "for (int g = tid; g < 0; g += NT)")],
     "noscale": [("const float sv = scale_fn(i >= H && i < H + NB ? raw + bias : raw);",
                  "const float sv = raw;")],
