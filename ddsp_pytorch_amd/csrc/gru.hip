@@ -20,19 +20,22 @@ namespace ddsp {
 namespace {
 
 constexpr int kHS = 4;    // hidden units per workgroup
-constexpr int kBS = 16;   // batch rows per workgroup (16: 7.7-7.9 us per step at config 2; 32: 8.4-8.5, 64: 11.9)
-constexpr int kKC = 32;   // k-chunks (threads per batch row)
-constexpr int kNT = kBS * kKC;
+// Tile shape (template arguments of both step kernels): kBS batch rows per workgroup x kKC k-chunks
+// (threads per batch row), kBS * kKC = 512 threads.  (16, 32) where hidden % 128 == 0 — 7.7-7.9 us per
+// step at config 2 against 8.4-8.5 for (32, 16) and 11.9 for (64, 8), profiles/r04i_gru_tiles.log —
+// else (32, 16) (hidden % 64 == 0).
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // grid (H / kHS, ceil(B / kBS)); LDS: W slice [3 kHS][H] + partials [kKC][3 kHS][kBS]
-__global__ void __launch_bounds__(kNT) gru_step_kernel(const float* __restrict__ xp, const float* __restrict__ w_hh,
+template <int kBS, int kKC>
+__global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __restrict__ xp, const float* __restrict__ w_hh,
                                                        const float* __restrict__ b_hh, const float* __restrict__ h_prev,
                                                        int64_t hp_ld, float* __restrict__ h_out, int64_t ho_ld,
                                                        int B, int H, int64_t xp_ld, float* __restrict__ save,
                                                        int64_t save_plane, float* __restrict__ h_copy) {
   extern __shared__ float smem[];
+  constexpr int kNT = kBS * kKC;
   constexpr int R = 3 * kHS;
   float* W = smem;                    // [R][H]
   float* part = smem + R * H;         // [kKC][R][kBS]
@@ -184,12 +187,14 @@ __global__ void gru_bwd_init_kernel(const float* __restrict__ dout, const float*
 // step t (>= 1): dh_{t-1} for units [i0, i0+kHS) x a batch tile, then step t-1's elementwise
 // part; t == 0 writes dh0 only.  grid (H / kHS, ceil(B / kBS)); LDS: W_hh columns [3H][kHS] +
 // partials [kKC][kHS][kBS]
-__global__ void __launch_bounds__(kNT) gru_bwd_step_kernel(
+template <int kBS, int kKC>
+__global__ void __launch_bounds__(kBS * kKC) gru_bwd_step_kernel(
     const float* __restrict__ w_t, const float* __restrict__ save, int64_t plane, const float* __restrict__ dout,
     const float* __restrict__ out, const float* __restrict__ h0, float* __restrict__ dxp, float* __restrict__ dgn,
     const float* __restrict__ dh_in, float* __restrict__ dh_outbuf, float* __restrict__ dh0, int B, int T, int H,
     int t) {
   extern __shared__ float smem[];
+  constexpr int kNT = kBS * kKC;
   const int K = 3 * H;
   float* Wt = smem;                 // [K][kHS]: Wt[k][u] = W_hh[k][i0 + u]
   float* part = smem + K * kHS;     // [kKC][kHS][kBS]
@@ -285,12 +290,27 @@ using namespace ddsp;
 
 extern "C" {
 
-int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
-                         float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
-  if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
-  if (batch == 0 || steps == 0) return DDSP_HIP_OK;
-  if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
-  if (hidden % (4 * kKC) || hidden % kHS || hidden > 4096 || batch > 65535 * kBS) return DDSP_HIP_ERANGE;
+}  // extern "C"
+
+template <int kBS, int kKC>
+static int gru_backward_steps(const float* w_t, const float* gates, int64_t plane, const float* grad_out, const float* out,
+                              const float* h0, float* grad_xp, float* grad_gn, float* const* dhb, float* grad_h0, int B,
+                              int T, int H, hipStream_t st) {
+  const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)kKC * kHS * kBS);
+  const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
+  for (int t = T - 1; t >= 0; --t) {
+    hipLaunchKernelGGL((gru_bwd_step_kernel<kBS, kKC>), grid, dim3(kBS * kKC), shm, st, w_t, gates, plane, grad_out, out,
+                       h0, grad_xp, grad_gn, dhb[t & 1], dhb[(t - 1) & 1], grad_h0, B, T, H, t);
+    int r = launch_status();
+    if (r) return r;
+  }
+  return DDSP_HIP_OK;
+}
+
+template <int kBS, int kKC>
+static int gru_forward_launch(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
+                              float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
+  if (batch > 65535 * kBS) return DDSP_HIP_ERANGE;
   const int H = (int)hidden, B = (int)batch;
   const size_t shm = sizeof(float) * ((size_t)3 * kHS * H + (size_t)kKC * 3 * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
@@ -300,7 +320,7 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   for (int64_t t = 0; t < steps; ++t) {
     const float* hp = t == 0 ? h0 : out + (t - 1) * hidden;
     const int64_t hp_ld = t == 0 ? hidden : row;
-    hipLaunchKernelGGL(gru_step_kernel, grid, dim3(kNT), shm, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL((gru_step_kernel<kBS, kKC>), grid, dim3(kBS * kKC), shm, reinterpret_cast<hipStream_t>(stream),
                        xp + t * 3 * hidden, w_hh, b_hh, hp, hp_ld, out + t * hidden, row, B, H, steps * 3 * hidden,
                        gates ? gates + t * hidden : nullptr, batch * steps * hidden,
                        direct && t == steps - 1 ? h_last : nullptr);
@@ -316,6 +336,19 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   return DDSP_HIP_OK;
 }
 
+extern "C" {
+
+int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
+                         float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
+  if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || steps == 0) return DDSP_HIP_OK;
+  if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
+  if (hidden % 64 || hidden > 4096) return DDSP_HIP_ERANGE;
+  if (hidden % 128 == 0)
+    return gru_forward_launch<16, 32>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
+  return gru_forward_launch<32, 16>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
+}
+
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden) {
   if (batch < 1 || hidden < 1) return 0;
   return sizeof(float) * ((size_t)2 * batch * hidden + (size_t)3 * hidden * hidden);
@@ -328,7 +361,7 @@ int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* ou
   if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!w_hh || !gates || !out || !grad_xp || !grad_gn) return DDSP_HIP_EINVAL;
-  if (hidden % (4 * kKC) || hidden % kHS || hidden > 4096 || batch > 65535 * kBS) return DDSP_HIP_ERANGE;
+  if (hidden % 64 || hidden > 4096 || batch > 65535 * 16) return DDSP_HIP_ERANGE;
   if (!workspace || workspace_bytes < ddsp_hip_gru_backward_workspace_size(batch, hidden)) return DDSP_HIP_EWORKSPACE;
   const int H = (int)hidden, B = (int)batch, T = (int)steps;
   const int64_t plane = batch * steps * hidden;
@@ -342,12 +375,12 @@ int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* ou
                      grad_xp, grad_gn, dhb[(T - 1) & 1], B, T, H);
   int r = launch_status();
   if (r) return r;
-  const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)kKC * kHS * kBS);
-  const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
-  for (int t = T - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(gru_bwd_step_kernel, grid, dim3(kNT), shm, st, w_t, gates, plane, grad_out, out, h0, grad_xp,
-                       grad_gn, dhb[t & 1], dhb[(t - 1) & 1], grad_h0, B, T, H, t);
-    if ((r = launch_status())) return r;
+  if (H % 128 == 0) {
+    if ((r = gru_backward_steps<16, 32>(w_t, gates, plane, grad_out, out, h0, grad_xp, grad_gn, dhb, grad_h0, B, T, H, st)))
+      return r;
+  } else if ((r = gru_backward_steps<32, 16>(w_t, gates, plane, grad_out, out, h0, grad_xp, grad_gn, dhb, grad_h0, B, T,
+                                             H, st))) {
+    return r;
   }
   return DDSP_HIP_OK;
 }

@@ -17,8 +17,10 @@ CSRC = os.path.join(ROOT, "ddsp_pytorch_amd", "csrc")
 # name -> [(literal, replacement)]; every literal must occur in the source
 STEM = {"gru8": "gru", "gru16h2": "gru", "gru16h8": "gru", "gru32": "gru"}
 PROBES = {
-    "gru8": [("constexpr int kBS = 16;", "constexpr int kBS = 8;"), ("constexpr int kKC = 32;", "constexpr int kKC = 64;")],
-    "gru32": [("constexpr int kBS = 16;", "constexpr int kBS = 32;"), ("constexpr int kKC = 32;", "constexpr int kKC = 16;")],
+    "gru8": [("gru_forward_launch<16, 32>", "gru_forward_launch<8, 64>"),
+             ("gru_backward_steps<16, 32>", "gru_backward_steps<8, 64>")],
+    "gru32": [("gru_forward_launch<16, 32>", "gru_forward_launch<32, 16>"),
+              ("gru_backward_steps<16, 32>", "gru_backward_steps<32, 16>")],
     "gru16h2": [("constexpr int kHS = 4;", "constexpr int kHS = 2;")],
     "gru16h8": [("constexpr int kHS = 4;", "constexpr int kHS = 8;")],
     "noprefix": [("for (int g = tid; g < f; g += NT)", "for (int g = tid; g < 0; g += NT)")],
