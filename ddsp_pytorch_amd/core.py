@@ -542,6 +542,36 @@ def gru(x, gru_module, h0=None):
     return out, h_last
 
 
+def mlp_block(x, linear, norm, act, out=None, extras=()):
+    """ddsp/core.py:122-129, one whole block: LeakyReLU(LayerNorm(linear(x))) in one launch
+    (ddsp_hip_mlp_block: the Linear on the fp32 matrix cores, LayerNorm + LeakyReLU in its epilogue).
+    ``extras``: up to two [..., 1] tensors that are the Linear's LAST input features (the decoder's
+    out_mlp input [gru_out, f0, loudness], decoder.py:68, given as x = gru_out, extras = (f0, loudness)).
+    Returns None where the kernel does not apply (512 output features, 16-byte aligned output rows);
+    inference only."""
+    _dev(x, linear.weight, linear.bias, norm.weight, norm.bias, *extras)
+    n_out, n_in = linear.weight.shape
+    K = x.shape[-1]
+    if (len(extras) > 2 or K + len(extras) != n_in or n_out != 512 or tuple(norm.normalized_shape) != (n_out,)
+            or any(e.shape != x.shape[:-1] + (1,) for e in extras)):
+        return None
+    xc = _c(x)
+    lead = tuple(x.shape[:-1])
+    rows = xc.numel() // K if K else 0
+    if out is None:
+        out = torch.empty(*lead, n_out, dtype=torch.float32, device=x.device)
+    elif (tuple(out.shape) != lead + (n_out,) or out.stride(-1) != 1 or
+          any(out.stride(i) != out.stride(i + 1) * out.shape[i + 1] for i in range(out.dim() - 2))):
+        return None
+    y_ld = out.stride(-2) if out.dim() >= 2 else n_out
+    ec = [_c(e) for e in extras]
+    st = _lib.call("mlp_block", _lib.ptr(xc), K, K, _lib.ptr(_c(linear.weight)), n_in, _lib.ptr(_c(linear.bias)),
+                   _lib.ptr(ec[0] if ec else None), _lib.ptr(ec[1] if len(ec) > 1 else None), 1,
+                   _lib.ptr(_c(norm.weight)), _lib.ptr(_c(norm.bias)), float(norm.eps), float(act.negative_slope),
+                   _lib.ptr(out), int(y_ld), int(rows), n_out, _lib.stream_of(out), allow=(ERANGE,))
+    return None if st == ERANGE else out
+
+
 def layer_norm_leaky_relu(h, norm, act, out=None, w1=None, b1=None):
     """ddsp/core.py:122-129 after one block's Linear: LeakyReLU(LayerNorm(h)) in one pass
     (ddsp_hip_layer_norm_leaky_relu).  h [..., cols] contiguous; or, with w1/b1 (a Linear with one input

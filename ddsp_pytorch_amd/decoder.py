@@ -73,12 +73,16 @@ def _mlp_fusable(seq, x):
     return True
 
 
-def mlp_forward(seq, x, out=None):
-    """seq(x) for a core.py:122-129 MLP; on the GPU at inference each block's LayerNorm + LeakyReLU is one
-    kernel (core.layer_norm_leaky_relu) after the Linear's GEMM, a one-feature first Linear folds into it,
-    and the last block may write into ``out`` (e.g. a column slice of the GRU input concatenation)."""
+def mlp_forward(seq, x, out=None, extras=()):
+    """seq(torch.cat([x, *extras], -1)) for a core.py:122-129 MLP.  On the GPU at inference a block with
+    512 outputs is ONE launch (core.mlp_block: the Linear on the matrix cores, LayerNorm + LeakyReLU in
+    its epilogue; ``extras`` — per-row [..., 1] inputs appended to x, the out_mlp's f0 and loudness —
+    enter the first block's epilogue, so the concatenation is never built), a one-feature first Linear
+    folds into the LayerNorm kernel (core.layer_norm_leaky_relu), other blocks run their GEMM then that
+    kernel; the last block may write into ``out`` (e.g. a column slice of the GRU input concatenation)."""
     if not _mlp_fusable(seq, x):
-        y = seq(x)
+        xin = torch.cat([x, *extras], -1) if extras else x
+        y = seq(xin)
         if out is None:
             return y
         out.copy_(y)
@@ -88,12 +92,15 @@ def mlp_forward(seq, x, out=None):
     for i in range(0, len(mods), 3):
         lin, ln, act = mods[i:i + 3]
         dst = out if i + 3 == len(mods) else None
-        if lin.in_features == 1:
+        ext = extras if i == 0 else ()
+        y = None
+        if lin.in_features == 1 and not ext:
             y = core.layer_norm_leaky_relu(h, ln, act, out=dst, w1=lin.weight[:, 0], b1=lin.bias)
-            if y is None:
-                y = act(ln(lin(h)))
-        else:
-            g = torch.nn.functional.linear(h, lin.weight, lin.bias)
+        elif lin.in_features >= 16:
+            y = core.mlp_block(h, lin, ln, act, out=dst, extras=ext)
+        if y is None:
+            hin = torch.cat([h, *ext], -1) if ext else h
+            g = torch.nn.functional.linear(hin, lin.weight, lin.bias)
             y = core.layer_norm_leaky_relu(g, ln, act, out=dst)
             if y is None:
                 y = act(ln(g))
@@ -126,7 +133,7 @@ def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
         self.cache_gru.copy_(cache)
     else:
         gru_out = _gru(self, hidden, None)[0]
-    return mlp_forward(self.out_mlp, torch.cat([gru_out, f0, loudness], -1))
+    return mlp_forward(self.out_mlp, gru_out, extras=(f0, loudness))
 
 
 def _hooked(m):

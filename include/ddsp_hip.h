@@ -229,6 +229,15 @@ int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, 
  * h = x[r] * w1 + b1 formed on the fly.  gamma/beta: the LayerNorm's affine; eps and the negative
  * slope as in torch (1e-5, 0.01).  y [rows, y_ld] may be a column slice of a wider buffer.  One pass
  * instead of torch's two; cols 512 or 1024 with 16-byte aligned rows, else DDSP_HIP_ERANGE. */
+/* ddsp/core.py:122-129: one whole MLP block, y = LeakyReLU(LayerNorm(x W^T + b)), W [out, w_ld] the
+ * nn.Linear weight, for out_features = 512 (else DDSP_HIP_ERANGE): the Linear on the fp32 matrix cores,
+ * LayerNorm + LeakyReLU in its epilogue.  e0/e1 (nullable, per-row scalars at stride e_ld) add
+ * e0[r] W[:, in] + e1[r] W[:, in + 1] — the decoder's out_mlp input [gru_out, f0, loudness]
+ * (decoder.py:68) without the concatenation.  y [rows, y_ld] may be a column slice. */
+int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
+                       const float* bias, const float* e0, const float* e1, int64_t e_ld, const float* gamma,
+                       const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
+                       int64_t out_features, void* stream);
 int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1, const float* b1, const float* gamma,
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);

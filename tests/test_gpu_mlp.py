@@ -58,3 +58,39 @@ def test_mlp_under_autograd_keeps_torch(dd):
     assert not _mlp_fusable(m, x)
     with torch.no_grad():
         assert _mlp_fusable(m, x)
+
+
+@pytest.mark.parametrize("rows", [1, 63, 64, 65, 1000])
+@pytest.mark.parametrize("in_size", [512, 33])
+def test_mlp_block_kernel(dd, rows, in_size):
+    """core.mlp_block (Linear on the matrix cores + LayerNorm + LeakyReLU epilogue) against torch's
+    modules: row counts around the 64-row workgroup tile, K not a multiple of the 16-wide K-step."""
+    torch.manual_seed(rows + in_size)
+    lin = torch.nn.Linear(in_size, 512).cuda()
+    ln = torch.nn.LayerNorm(512).cuda()
+    act = torch.nn.LeakyReLU()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+        x = torch.randn(rows, in_size, device="cuda") * 2.0
+        y = dd.core.mlp_block(x, lin, ln, act)
+        torch.testing.assert_close(y, act(ln(lin(x))), rtol=2e-5, atol=2e-5)
+
+
+def test_mlp_forward_extras_match_cat(dd):
+    """The decoder's out_mlp input [gru_out, f0, loudness] (decoder.py:68) given as x + two per-row
+    extras: the same result as torch's modules on the concatenation, with no concatenation built."""
+    from ddsp_pytorch_amd.decoder import mlp, mlp_forward
+    torch.manual_seed(3)
+    m = mlp(514, 512, 3).cuda().eval()
+    gru_out = torch.randn(5, 101, 512, device="cuda")
+    f0 = torch.rand(5, 101, 1, device="cuda") * 800 + 50
+    loud = torch.randn(5, 101, 1, device="cuda") * 4
+    with torch.no_grad():
+        ref = m(torch.cat([gru_out, f0, loud], -1))
+        got = mlp_forward(m, gru_out, extras=(f0, loud))
+    torch.testing.assert_close(got, ref, rtol=2e-5, atol=2e-5)
+    # outside the kernel's shapes (1024 outputs): None, the caller keeps the GEMM + LayerNorm route
+    big = mlp(512, 1024, 1).cuda()
+    with torch.no_grad():
+        assert dd.core.mlp_block(gru_out, big[0], big[1], big[2]) is None

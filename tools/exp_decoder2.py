@@ -1,7 +1,9 @@
 """Development experiment: where DDSPDecoder.forward's time goes at config 2 (B=64, F=200, hidden 512) —
 host-timed pieces (after warmup) and, under rocprofv3 --kernel-trace, the kernels of each piece.
 
-    python tools/exp_decoder2.py [piece ...]   pieces: net gru mlps dsyn proj synth fwd
+    python tools/exp_decoder2.py [piece ...]   pieces: net gru mlps outmlp outmlp_gemm net_gemm dsyn proj synth fwd
+(outmlp: the out_mlp through decoder.mlp_forward, each block one core.mlp_block launch; *_gemm: the same
+with core.mlp_block disabled, i.e. the GEMM + fused LayerNorm/LeakyReLU route)
 """
 import json
 import os
@@ -12,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from ddsp_pytorch_amd import core  # noqa: E402
-from ddsp_pytorch_amd.decoder import DDSPDecoder, decoder_projections, decoder_synthesize  # noqa: E402
+from ddsp_pytorch_amd.decoder import DDSPDecoder, decoder_projections, decoder_synthesize, mlp_forward  # noqa: E402
 
 dev = "cuda"
 B, F, bs, sr = 64, 200, 512, 48000
@@ -38,7 +40,19 @@ def t(fn, reps=20):
     return {"ms": round((time.perf_counter() - t0 - host) / reps * 1e3, 4), "host_ms_one_call": round(host * 1e3, 4)}
 
 
-pieces = sys.argv[1:] or ["net", "gru", "mlps", "dsyn", "proj", "synth", "fwd"]
+pieces = sys.argv[1:] or ["net", "gru", "mlps", "outmlp", "outmlp_gemm", "net_gemm", "dsyn", "proj", "synth", "fwd"]
+_block = core.mlp_block
+
+
+def gemm_route(fn):
+    def run():
+        core.mlp_block = lambda *a, **k: None
+        try:
+            return fn()
+        finally:
+            core.mlp_block = _block
+    return run
+
 res = {}
 with torch.no_grad():
     d = m.decoder
@@ -52,6 +66,14 @@ with torch.no_grad():
             res[p] = t(lambda: core.gru(hidden_in, d.gru, None))
         elif p == "mlps":
             res[p] = t(lambda: d.out_mlp(torch.cat([d.f0_mlp(f0), d.loudness_mlp(lo), f0, lo], -1)[..., :514]))
+        elif p == "outmlp":
+            g = core.gru(hidden_in, d.gru, None)[0]
+            res[p] = t(lambda: mlp_forward(d.out_mlp, g, extras=(f0, lo)))
+        elif p == "outmlp_gemm":
+            g = core.gru(hidden_in, d.gru, None)[0]
+            res[p] = t(gemm_route(lambda: mlp_forward(d.out_mlp, g, extras=(f0, lo))))
+        elif p == "net_gemm":
+            res[p] = t(gemm_route(lambda: m.decoder(f0, lo)))
         elif p == "dsyn":
             res[p] = t(lambda: decoder_synthesize(m, hidden, f0))
         elif p == "proj":
