@@ -547,7 +547,7 @@ def mlp_block(x, linear, norm, act, out=None, extras=()):
     (ddsp_hip_mlp_block: the Linear on the fp32 matrix cores, LayerNorm + LeakyReLU in its epilogue).
     ``extras``: up to two [..., 1] tensors that are the Linear's LAST input features (the decoder's
     out_mlp input [gru_out, f0, loudness], decoder.py:68, given as x = gru_out, extras = (f0, loudness)).
-    Returns None where the kernel does not apply (512 output features, 16-byte aligned output rows);
+    Returns None where the kernel does not apply (it is built for 512 output features);
     inference only."""
     _dev(x, linear.weight, linear.bias, norm.weight, norm.bias, *extras)
     n_out, n_in = linear.weight.shape

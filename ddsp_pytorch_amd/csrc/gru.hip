@@ -7,7 +7,9 @@
 // where xp = x W_ih^T + b_ih for every time step at once is one plain GEMM (the caller's
 // hipBLASLt matmul).  The recurrence is what MIOpen spends ~45 us per step on at batch 64,
 // hidden 512: here one launch per step, 512 workgroups (hidden slices of 4 units x batch tiles
-// of 16), each holding its 12 rows of W_hh in LDS and its batch tile's h chunk in registers;
+// of 16), each holding its 12 rows of W_hh in LDS and its batch tile's h chunk in registers; a
+// step is a chain of latencies (load h and W, reduce, gate), so all of a step's loads are in flight
+// together;
 // the kernel boundary is the step's grid-wide barrier (no persistent spin, no residency
 // requirement).  h_t is written straight into the output sequence, which is the next step's h.
 #include <hip/hip_runtime.h>
@@ -27,24 +29,35 @@ constexpr int kHS = 4;    // hidden units per workgroup
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// grid (H / kHS, ceil(B / kBS)); LDS: W slice [3 kHS][H] + partials [kKC][3 kHS][kBS]
-template <int kBS, int kKC>
+// grid (H / kHS, ceil(B / kBS)); LDS: W slice [3 kHS][H] + per-wave partials [kNT / 64][3 kHS][kBS].
+// A step is a chain of dependent latencies, not work (100 MFLOP per step at config 2), so every
+// global load is issued before the first wait: the epilogue operands, this thread's h chunk and its
+// share of the W slice (unpredicated, at clamped addresses; out-of-range values are never used),
+// then one wait, the W slice to LDS, one barrier.  The k-chunk partials are summed inside each wave
+// by lane exchanges first, so the epilogue wave reads kNT / 64 partials per gate instead of kKC.
+// kH: the hidden size as a compile-time constant (512, the decoder's) so that the loads carry no
+// predicates the compiler could turn into per-load branches and waits; 0 = any hidden size.
+template <int kBS, int kKC, int kH>
 __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __restrict__ xp, const float* __restrict__ w_hh,
                                                        const float* __restrict__ b_hh, const float* __restrict__ h_prev,
                                                        int64_t hp_ld, float* __restrict__ h_out, int64_t ho_ld,
-                                                       int B, int H, int64_t xp_ld, float* __restrict__ save,
+                                                       int B, int H_arg, int64_t xp_ld, float* __restrict__ save,
                                                        int64_t save_plane, float* __restrict__ h_copy) {
   extern __shared__ float smem[];
   constexpr int kNT = kBS * kKC;
   constexpr int R = 3 * kHS;
+  constexpr int kWaves = kNT / 64, kG = 64 / kBS;  // waves; k-chunk groups per wave
+  static_assert(kBS <= 64 && 64 % kBS == 0 && kNT % 64 == 0, "tile shape");
+  constexpr int kWV = 4;              // W slice float4s per thread per staging round
+  const int H = kH ? kH : H_arg;
   float* W = smem;                    // [R][H]
-  float* part = smem + R * H;         // [kKC][R][kBS]
+  float* part = smem + R * H;         // [kWaves][R][kBS]
   const int j0 = blockIdx.x * kHS, b0 = blockIdx.y * kBS;
   const int tid = threadIdx.x;
   const int bl = tid % kBS, c = tid / kBS;
   const int b = b0 + bl;
   const int KLr = H / kKC;  // this thread's k range [c*KLr, (c+1)*KLr), a multiple of 4
-  // the gate epilogue's operands, loaded up front so their latency hides under the dot products
+  // the gate epilogue's operands
   const int eu = tid / kBS, ebb = tid - eu * kBS;
   const int ebi = b0 + ebb, ej = j0 + eu;
   const bool epi = tid < kHS * kBS && ebi < B;
@@ -59,25 +72,37 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
     eb_n = b_hh[2 * H + ej];
     ehp = h_prev ? h_prev[(int64_t)ebi * hp_ld + ej] : 0.0f;
   }
-  const bool hv_ok = h_prev && b < B;
-  const float* hrow = h_prev + (int64_t)(hv_ok ? b : 0) * hp_ld + c * KLr;
+  const bool hv_ok = h_prev != nullptr;  // uniform: no h0 at step 0 means h = 0 (then W is read instead)
+  const float* hrow = hv_ok ? h_prev + (int64_t)(b < B ? b : B - 1) * hp_ld + c * KLr : w_hh + c * KLr;  // rows >= B: never stored
+  const int n4 = R * H / 4;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
   for (int k0 = 0; k0 < KLr; k0 += 32) {
-    // issue up to 8 16-B h loads first (the first batch overlaps the W staging below)
     float4 hv[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      hv[q] = (hv_ok && k0 + 4 * q < KLr) ? *reinterpret_cast<const float4*>(hrow + k0 + 4 * q)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < 8; ++q) {
+      const int kk = k0 + 4 * q < KLr ? k0 + 4 * q : KLr - 4;
+      hv[q] = *reinterpret_cast<const float4*>(hrow + kk);
+      if (!hv_ok) hv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (k0 == 0) {
       // rows: gate g of unit u is W_hh row g*H + j0 + u
-      for (int i = tid; i < R * H / 4; i += kNT) {
-        const int r = (4 * i) / H, k = 4 * i - r * H;
-        const int g = r / kHS, u = r - g * kHS;
-        *reinterpret_cast<float4*>(W + r * H + k) =
-            *reinterpret_cast<const float4*>(w_hh + (int64_t)(g * H + j0 + u) * H + k);
+      for (int i0 = tid; i0 < n4; i0 += kWV * kNT) {
+        float4 wv[kWV];
+#pragma unroll
+        for (int v = 0; v < kWV; ++v) {
+          const int i = i0 + v * kNT < n4 ? i0 + v * kNT : n4 - 1;
+          const int r = (4 * i) / H, k = 4 * i - r * H;
+          const int g = r / kHS, u = r - g * kHS;
+          wv[v] = *reinterpret_cast<const float4*>(w_hh + (int64_t)(g * H + j0 + u) * H + k);
+        }
+#pragma unroll
+        for (int v = 0; v < kWV; ++v) {  // clamped indices rewrite the last element with its own value
+          const int i = i0 + v * kNT < n4 ? i0 + v * kNT : n4 - 1;
+          const int r = (4 * i) / H, k = 4 * i - r * H;
+          *reinterpret_cast<float4*>(W + r * H + k) = wv[v];
+        }
       }
       __syncthreads();
     }
@@ -92,17 +117,25 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
       }
     }
   }
+  // the kG k-chunks of each wave (lanes bl, bl + kBS, ...) summed by lane exchange; group g keeps rows r % kG == g
 #pragma unroll
-  for (int r = 0; r < R; ++r) part[(c * R + r) * kBS + bl] = acc[r];
+  for (int m = kBS; m < 64; m <<= 1)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += __shfl_xor(acc[r], m, 64);
+  const int wv_id = tid >> 6, grp = (tid & 63) / kBS;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (r % kG == grp) part[(wv_id * R + r) * kBS + bl] = acc[r];
   __syncthreads();
-  // gates for kHS units x kBS batch rows (128 items)
+  // gates for kHS units x kBS batch rows
   if (epi) {
     const int u = eu, bb = ebb;
     float hr = 0.f, hz = 0.f, hn = 0.f;
-    for (int cc = 0; cc < kKC; ++cc) {
-      hr += part[(cc * R + 0 * kHS + u) * kBS + bb];
-      hz += part[(cc * R + 1 * kHS + u) * kBS + bb];
-      hn += part[(cc * R + 2 * kHS + u) * kBS + bb];
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      hr += part[(w * R + 0 * kHS + u) * kBS + bb];
+      hz += part[(w * R + 1 * kHS + u) * kBS + bb];
+      hn += part[(w * R + 2 * kHS + u) * kBS + bb];
     }
     const float r = sigmoidf_(ex_r + (hr + eb_r));
     const float z = sigmoidf_(ex_z + (hz + eb_z));
@@ -119,7 +152,6 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
     }
   }
 }
-
 
 // ---------------------------------------------------------------------------------------
 // Backward (BPTT) of the recurrence, for training.  With dh the total gradient reaching h_t:
@@ -186,25 +218,30 @@ __global__ void gru_bwd_init_kernel(const float* __restrict__ dout, const float*
 
 // step t (>= 1): dh_{t-1} for units [i0, i0+kHS) x a batch tile, then step t-1's elementwise
 // part; t == 0 writes dh0 only.  grid (H / kHS, ceil(B / kBS)); LDS: W_hh columns [3H][kHS] +
-// partials [kKC][kHS][kBS]
-template <int kBS, int kKC>
+// per-wave partials [kNT / 64][kHS][kBS].  As in the forward step: every global load issued before
+// the first wait (kH = 512 makes the loop bounds compile-time constants), the k-chunk partials
+// summed inside each wave by lane exchanges.
+template <int kBS, int kKC, int kH>
 __global__ void __launch_bounds__(kBS * kKC) gru_bwd_step_kernel(
     const float* __restrict__ w_t, const float* __restrict__ save, int64_t plane, const float* __restrict__ dout,
     const float* __restrict__ out, const float* __restrict__ h0, float* __restrict__ dxp, float* __restrict__ dgn,
-    const float* __restrict__ dh_in, float* __restrict__ dh_outbuf, float* __restrict__ dh0, int B, int T, int H,
+    const float* __restrict__ dh_in, float* __restrict__ dh_outbuf, float* __restrict__ dh0, int B, int T, int H_arg,
     int t) {
   extern __shared__ float smem[];
   constexpr int kNT = kBS * kKC;
+  constexpr int kWaves = kNT / 64, kG = 64 / kBS;
+  static_assert(kBS <= 64 && 64 % kBS == 0 && kNT % 64 == 0 && (kHS % kG == 0 || kG % kHS == 0), "tile shape");
+  constexpr int kWV = 4;            // W columns' float4s per thread per staging round
+  const int H = kH ? kH : H_arg;
   const int K = 3 * H;
   float* Wt = smem;                 // [K][kHS]: Wt[k][u] = W_hh[k][i0 + u]
-  float* part = smem + K * kHS;     // [kKC][kHS][kBS]
+  float* part = smem + K * kHS;     // [kWaves][kHS][kBS]
   const int i0 = blockIdx.x * kHS, b0 = blockIdx.y * kBS;
   const int tid = threadIdx.x;
   const int bl = tid % kBS, c = tid / kBS;
   const int b = b0 + bl;
   const int KLr = K / kKC;  // this thread's reduction range (K % (4 kKC) == 0)
-  // the epilogue's operands (this step's z and dh, step t-1's saved gates, dout and h_{t-2}),
-  // loaded up front so their latency hides under the transposed product
+  // the epilogue's operands (this step's z and dh, step t-1's saved gates, dout and h_{t-2})
   const int eu = tid / kBS, ebb = tid - eu * kBS;
   const int ebi = b0 + ebb, ei = i0 + eu;
   const bool epi = tid < kHS * kBS && ebi < B;
@@ -223,54 +260,72 @@ __global__ void __launch_bounds__(kBS * kKC) gru_bwd_step_kernel(
       s_hn = save[3 * plane + eidx];
     }
   }
+  // this thread's dG_t chunk [c KLr, (c+1) KLr) of row b (rows >= B read row B-1 and are never stored)
+  const int bc = b < B ? b : B - 1;
+  const float* gx = dxp + ((int64_t)bc * T + t) * 3 * H;  // [3H]: r, z rows are dG
+  const float* gn = dgn + ((int64_t)bc * T + t) * H;      // [H]: dG_n
+  const int k0 = c * KLr;
+  const int n4 = kHS * K / 4;
   float acc[kHS];
 #pragma unroll
   for (int u = 0; u < kHS; ++u) acc[u] = 0.0f;
-  for (int e = tid; e < kHS * K / 4; e += kNT) {
-    const int u = e / (K / 4), k = 4 * (e - u * (K / 4));
-    const float4 v = *reinterpret_cast<const float4*>(w_t + (int64_t)(i0 + u) * K + k);
-    Wt[(k + 0) * kHS + u] = v.x;
-    Wt[(k + 1) * kHS + u] = v.y;
-    Wt[(k + 2) * kHS + u] = v.z;
-    Wt[(k + 3) * kHS + u] = v.w;
-  }
-  __syncthreads();
-  if (b < B) {
-    const float* gx = dxp + ((int64_t)b * T + t) * 3 * H;  // [3H]: r, z rows are dG
-    const float* gn = dgn + ((int64_t)b * T + t) * H;      // [H]: dG_n
-    const int k0 = c * KLr;
-    for (int kb = k0; kb < k0 + KLr; kb += 32) {
-      float4 g4[8];  // issue 8 16-B loads before consuming them
+  for (int kb = k0; kb < k0 + KLr; kb += 64) {
+    float4 g4[16];  // 16 16-B loads before consuming them (the first batch overlaps the W staging)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = kb + 4 * q;
-        g4[q] = k >= k0 + KLr ? make_float4(0.f, 0.f, 0.f, 0.f)
-                              : (k < 2 * H ? *reinterpret_cast<const float4*>(gx + k)
-                                           : *reinterpret_cast<const float4*>(gn + (k - 2 * H)));
+    for (int q = 0; q < 16; ++q) {
+      const int k = kb + 4 * q < k0 + KLr ? kb + 4 * q : k0 + KLr - 4;
+      g4[q] = *reinterpret_cast<const float4*>(k < 2 * H ? gx + k : gn + (k - 2 * H));
+    }
+    if (kb == k0) {
+      for (int e0 = tid; e0 < n4; e0 += kWV * kNT) {
+        float4 wv[kWV];
+#pragma unroll
+        for (int v = 0; v < kWV; ++v) {
+          const int e = e0 + v * kNT < n4 ? e0 + v * kNT : n4 - 1;
+          const int u = e / (K / 4), k = 4 * (e - u * (K / 4));
+          wv[v] = *reinterpret_cast<const float4*>(w_t + (int64_t)(i0 + u) * K + k);
+        }
+#pragma unroll
+        for (int v = 0; v < kWV; ++v) {  // clamped indices rewrite the last element with its own value
+          const int e = e0 + v * kNT < n4 ? e0 + v * kNT : n4 - 1;
+          const int u = e / (K / 4), k = 4 * (e - u * (K / 4));
+          Wt[(k + 0) * kHS + u] = wv[v].x;
+          Wt[(k + 1) * kHS + u] = wv[v].y;
+          Wt[(k + 2) * kHS + u] = wv[v].z;
+          Wt[(k + 3) * kHS + u] = wv[v].w;
+        }
       }
+      __syncthreads();
+    }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = kb + 4 * q;
-        if (k < k0 + KLr) {
-          const float gv[4] = {g4[q].x, g4[q].y, g4[q].z, g4[q].w};
+    for (int q = 0; q < 16; ++q) {
+      const int k = kb + 4 * q;
+      if (k < k0 + KLr) {
+        const float gv[4] = {g4[q].x, g4[q].y, g4[q].z, g4[q].w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float4 w = *reinterpret_cast<const float4*>(Wt + (k + e) * kHS);
-            acc[0] = fmaf(w.x, gv[e], acc[0]);
-            acc[1] = fmaf(w.y, gv[e], acc[1]);
-            acc[2] = fmaf(w.z, gv[e], acc[2]);
-            acc[3] = fmaf(w.w, gv[e], acc[3]);
-          }
+        for (int e = 0; e < 4; ++e) {
+          const float4 w = *reinterpret_cast<const float4*>(Wt + (k + e) * kHS);
+          acc[0] = fmaf(w.x, gv[e], acc[0]);
+          acc[1] = fmaf(w.y, gv[e], acc[1]);
+          acc[2] = fmaf(w.z, gv[e], acc[2]);
+          acc[3] = fmaf(w.w, gv[e], acc[3]);
         }
       }
     }
   }
 #pragma unroll
-  for (int u = 0; u < kHS; ++u) part[(c * kHS + u) * kBS + bl] = acc[u];
+  for (int m = kBS; m < 64; m <<= 1)
+#pragma unroll
+    for (int u = 0; u < kHS; ++u) acc[u] += __shfl_xor(acc[u], m, 64);
+  const int wv_id = tid >> 6, grp = (tid & 63) / kBS;
+#pragma unroll
+  for (int u = 0; u < kHS; ++u)
+    if (u % kG == grp % kHS) part[(wv_id * kHS + u) * kBS + bl] = acc[u];
   __syncthreads();
   if (epi) {
     float s = 0.0f;
-    for (int cc = 0; cc < kKC; ++cc) s += part[(cc * kHS + eu) * kBS + ebb];
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += part[(w * kHS + eu) * kBS + ebb];
     // dh_{t-1} = dh_t z_t + W_hh^T dG_t + dout_{t-1}
     float dh = e_dh * e_z + s;
     if (t == 0) {
@@ -292,14 +347,14 @@ extern "C" {
 
 }  // extern "C"
 
-template <int kBS, int kKC>
+template <int kBS, int kKC, int kH = 0>
 static int gru_backward_steps(const float* w_t, const float* gates, int64_t plane, const float* grad_out, const float* out,
                               const float* h0, float* grad_xp, float* grad_gn, float* const* dhb, float* grad_h0, int B,
                               int T, int H, hipStream_t st) {
-  const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)kKC * kHS * kBS);
+  const size_t shm = sizeof(float) * ((size_t)3 * H * kHS + (size_t)(kBS * kKC / 64) * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
   for (int t = T - 1; t >= 0; --t) {
-    hipLaunchKernelGGL((gru_bwd_step_kernel<kBS, kKC>), grid, dim3(kBS * kKC), shm, st, w_t, gates, plane, grad_out, out,
+    hipLaunchKernelGGL((gru_bwd_step_kernel<kBS, kKC, kH>), grid, dim3(kBS * kKC), shm, st, w_t, gates, plane, grad_out, out,
                        h0, grad_xp, grad_gn, dhb[t & 1], dhb[(t - 1) & 1], grad_h0, B, T, H, t);
     int r = launch_status();
     if (r) return r;
@@ -307,12 +362,12 @@ static int gru_backward_steps(const float* w_t, const float* gates, int64_t plan
   return DDSP_HIP_OK;
 }
 
-template <int kBS, int kKC>
+template <int kBS, int kKC, int kH = 0>
 static int gru_forward_launch(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                               float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {
   if (batch > 65535 * kBS) return DDSP_HIP_ERANGE;
   const int H = (int)hidden, B = (int)batch;
-  const size_t shm = sizeof(float) * ((size_t)3 * kHS * H + (size_t)kKC * 3 * kHS * kBS);
+  const size_t shm = sizeof(float) * ((size_t)3 * kHS * H + (size_t)(kBS * kKC / 64) * 3 * kHS * kBS);
   const dim3 grid((unsigned)(H / kHS), (unsigned)((B + kBS - 1) / kBS));
   const int64_t row = steps * hidden;  // out[b] row stride: [B, T, H]
   // h_T goes to h_last from the last step's kernel, unless that step still reads h0 = h_last
@@ -320,7 +375,7 @@ static int gru_forward_launch(const float* xp, const float* w_hh, const float* b
   for (int64_t t = 0; t < steps; ++t) {
     const float* hp = t == 0 ? h0 : out + (t - 1) * hidden;
     const int64_t hp_ld = t == 0 ? hidden : row;
-    hipLaunchKernelGGL((gru_step_kernel<kBS, kKC>), grid, dim3(kBS * kKC), shm, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL((gru_step_kernel<kBS, kKC, kH>), grid, dim3(kBS * kKC), shm, reinterpret_cast<hipStream_t>(stream),
                        xp + t * 3 * hidden, w_hh, b_hh, hp, hp_ld, out + t * hidden, row, B, H, steps * 3 * hidden,
                        gates ? gates + t * hidden : nullptr, batch * steps * hidden,
                        direct && t == steps - 1 ? h_last : nullptr);
@@ -344,6 +399,8 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
   if (hidden % 64 || hidden > 4096) return DDSP_HIP_ERANGE;
+  if (hidden == 512)
+    return gru_forward_launch<16, 32, 512>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
   if (hidden % 128 == 0)
     return gru_forward_launch<16, 32>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
   return gru_forward_launch<32, 16>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
@@ -375,7 +432,11 @@ int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* ou
                      grad_xp, grad_gn, dhb[(T - 1) & 1], B, T, H);
   int r = launch_status();
   if (r) return r;
-  if (H % 128 == 0) {
+  if (H == 512) {
+    if ((r = gru_backward_steps<16, 32, 512>(w_t, gates, plane, grad_out, out, h0, grad_xp, grad_gn, dhb, grad_h0, B, T, H,
+                                             st)))
+      return r;
+  } else if (H % 128 == 0) {
     if ((r = gru_backward_steps<16, 32>(w_t, gates, plane, grad_out, out, h0, grad_xp, grad_gn, dhb, grad_h0, B, T, H, st)))
       return r;
   } else if ((r = gru_backward_steps<32, 16>(w_t, gates, plane, grad_out, out, h0, grad_xp, grad_gn, dhb, grad_h0, B, T,

@@ -1,6 +1,6 @@
 """Run one kernel of the synthesis path repeatedly at configuration 2 (for rocprofv3 PMC passes).
 
-    python tools/kernel_probe.py {fused,bwd,reverb_bwd,gru,harmonic,harmonic_frames,noise,reverb,op} [reps]
+    python tools/kernel_probe.py {fused,bwd,reverb_bwd,gru,gru_train,harmonic,harmonic_frames,noise,reverb,op} [reps]
 """
 import os
 import sys
@@ -35,6 +35,15 @@ def main():
         with torch.no_grad():
             for _ in range(reps):
                 core.gru(xg, g)
+        torch.cuda.synchronize()
+        return
+    if which == "gru_train":  # the same recurrence under autograd: forward step kernels + BPTT step kernels
+        torch.manual_seed(0)
+        g = torch.nn.GRU(1024, 512, batch_first=True).to(dev)
+        xg = torch.randn(B, F, 1024, device=dev, requires_grad=True)
+        for _ in range(reps):
+            out, _h = core.gru(xg, g)
+            out.sum().backward()
         torch.cuda.synchronize()
         return
     if which == "reverb_bwd":  # the UPOLS backward (input and IR gradients)
