@@ -2,11 +2,12 @@
 state_dict keys (ddsp/models/decoder.py:9-136, ddsp/core.py:122-133), wired to the gfx950
 synth modules.
 
-The GRU/MLP control network is plain PyTorch (MIOpen/hipBLASLt underneath) — it is not
-part of the accelerated synthesis path.  It exists so that a
-reference checkpoint can be loaded and run end to end on the device, and so the
-synthesis section of ``forward`` (decoder.py:106-125) can be exercised exactly as the
-reference calls it.
+The control network before the path runs at inference on gfx950 kernels
+too: each MLP block is one matrix-core launch with its LayerNorm + LeakyReLU (core.mlp_block), the
+GRU recurrence is the step kernel (core.gru; its input projection a hipBLASLt GEMM), the two
+projections one matrix-core Linear (core.linear), and the synthesis section of ``forward``
+(decoder.py:106-125) one fused launch before the reverb.  Under autograd the MLPs and projections
+keep torch's modules; the GRU's BPTT runs on its backward step kernel.
 """
 import torch
 import torch.nn as nn
@@ -184,7 +185,7 @@ def _shared_projection(self):
 
 
 def decoder_projections(self, hidden):
-    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE GEMM over the
+    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE Linear over the
     two projections' weights held in one shared buffer (``_shared_projection``; the two outputs are column
     slices of it, which the fused synthesis kernel reads with their row stride).  Under autograd the
     concatenation is differentiable, so the parameters receive their gradients as the reference's do."""
@@ -194,9 +195,12 @@ def decoder_projections(self, hidden):
     ps = (hp.weight, hp.bias, npj.weight, npj.bias)
     if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
         w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
-    else:
+        out = torch.nn.functional.linear(hidden, w, b)
+    else:  # inference: one launch of the matrix-core Linear (core.linear), else the library GEMM
         w, b = _shared_projection(self)
-    out = torch.nn.functional.linear(hidden, w, b)
+        out = core.linear(hidden, w, b)
+        if out is None:
+            out = torch.nn.functional.linear(hidden, w, b)
     h1 = hp.out_features
     return out[..., :h1], out[..., h1:]
 
