@@ -542,22 +542,6 @@ def gru(x, gru_module, h0=None):
     return out, h_last
 
 
-def linear(x, weight, bias):
-    """torch.nn.functional.linear(x, weight, bias) for up to 192 output features on the fp32 matrix
-    cores (ddsp_hip_linear): the decoder's two projections (decoder.py:107-108) stacked into one.
-    Returns None where the kernel does not apply (more outputs, no bias); inference only."""
-    _dev(x, weight)
-    if bias is None or weight.dim() != 2 or weight.shape[1] != x.shape[-1] or bias.shape != weight.shape[:1]:
-        return None
-    n_out, K = weight.shape
-    xc = _c(x)
-    rows = xc.numel() // K if K else 0
-    out = torch.empty(*x.shape[:-1], n_out, dtype=torch.float32, device=x.device)
-    st = _lib.call("linear", _lib.ptr(xc), K, K, _lib.ptr(_c(weight)), K, _lib.ptr(_c(bias)), _lib.ptr(out), n_out,
-                   int(rows), n_out, _lib.stream_of(out), allow=(ERANGE,))
-    return None if st == ERANGE else out
-
-
 def mlp_block(x, linear, norm, act, out=None, extras=()):
     """ddsp/core.py:122-129, one whole block: LeakyReLU(LayerNorm(linear(x))) in one launch
     (ddsp_hip_mlp_block: the Linear on the fp32 matrix cores, LayerNorm + LeakyReLU in its epilogue).

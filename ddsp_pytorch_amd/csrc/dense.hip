@@ -235,193 +235,179 @@ __global__ void __launch_bounds__(256) ln_leaky_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Linears at full batch on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products and
-// sums), y = x W^T + b, one workgroup per 16 kRT rows x 64 kNW output columns (kNW waves, each 64
-// columns as kRT x 4 MFMA tiles of 16 x 16); x and W stream through LDS in K-steps of 16
-// (double-buffered, one barrier per step).  Within a K-step lane l supplies k = 4 (l >> 4) + s at
-// sub-step s for both operands (one ds_read_b128 per operand tile), so every product pairs x[r][k]
-// with W[c][k].  Two epilogues:
-//  * kLN (one MLP block, ddsp/core.py:122-129, 512 outputs = the whole row in one workgroup):
-//    LayerNorm + LeakyReLU, so the block's [rows, 512] result is written once (hipBLASLt's GEMM wrote
-//    it, then LayerNorm and LeakyReLU re-read and re-wrote it); e0/e1 (optional): per-row scalars with
-//    weight columns K and K + 1 — the decoder's out_mlp input [gru_out, f0, loudness] (decoder.py:68)
-//    without materialising the concatenation;
-//  * plain (the decoder's two projections stacked, decoder.py:107-108: 166 outputs at config 2):
-//    bias added, columns >= N neither loaded nor stored.
-constexpr int kMlpKC = 16;          // K per LDS stage
+// One whole MLP block at full batch (ddsp/core.py:122-129): y = LeakyReLU(LayerNorm(x W^T + b)) for
+// 512 output features, the Linear on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
+// products and sums) and LayerNorm + LeakyReLU in the epilogue, so the block's [rows, 512] result is
+// written once (hipBLASLt's GEMM wrote it, then LayerNorm and LeakyReLU re-read and re-wrote it).
+// A workgroup owns 64 full rows (LayerNorm needs whole rows), its 8 waves 64 output columns each as a
+// 4 x 4 grid of 16 x 16 MFMA tiles.  x and W stream through ONE LDS stage of K = 32 per step: the
+// next step's operands are loaded into registers at the top of a step and written to LDS after its
+// 128 MFMAs per wave, so each load's latency hides under a whole step of matrix work (a 16-wide,
+// double-buffered LDS stage left the loads exposed: 103 us per config-2 block, against 55 us of
+// MFMA issue).  Within a step lane l supplies k = 16 h + 4 (l >> 4) + s at sub-step (h, s) for both
+// operands (one ds_read_b128 per operand tile per half), so every product pairs x[r][k] with W[c][k].
+// kVec: 16-byte row loads (x and W rows 16-B aligned, K % 4 == 0), else scalar loads.  e0/e1
+// (optional): per-row scalars with weight columns K and K + 1 — the decoder's out_mlp input
+// [gru_out, f0, loudness] (decoder.py:68) without materialising the concatenation.
+constexpr int kMlpN = 512;          // output features (8 waves x 64)
+constexpr int kMlpRows = 64;        // rows per workgroup
+constexpr int kMlpKC = 32;          // K per LDS stage
 constexpr int kMlpLd = kMlpKC + 4;  // LDS row stride (floats): 16-B aligned rows, banks spread
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int kNW, int kRT, bool kLN>
-__global__ void __launch_bounds__(64 * kNW) mfma_rows_kernel(
+template <bool kVec>
+__global__ void __launch_bounds__(512) mlp_block_kernel(
     const float* __restrict__ x, int64_t x_ld, int K, const float* __restrict__ w, int64_t w_ld,
     const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float slope, float* __restrict__ y,
-    int64_t y_ld, int64_t R, int N) {
-  constexpr int kNT = 64 * kNW, kN = 64 * kNW, kRows = 16 * kRT;
-  constexpr int kXA = kRows * kMlpKC / kNT;  // x values per thread per K-step
-  static_assert(kRows * kMlpKC % kNT == 0, "x tile must split evenly over the threads");
-  __shared__ __attribute__((aligned(16))) float As[2][kRows * kMlpLd];
-  __shared__ __attribute__((aligned(16))) float Bs[2][kN * kMlpLd];
+    int64_t y_ld, int64_t R) {
+  __shared__ __attribute__((aligned(16))) float As[kMlpRows * kMlpLd];
+  __shared__ __attribute__((aligned(16))) float Bs[kMlpN * kMlpLd];
+  __shared__ float red[8][kMlpRows];
+  __shared__ float stat[kMlpRows];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int q = lane >> 4, l16 = lane & 15;
-  const int64_t r0 = (int64_t)blockIdx.x * kRows;
+  const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
   const int nc = (K + kMlpKC - 1) / kMlpKC;
-  float sa[kXA], sb[16];
-  auto load = [&](int c) {  // this thread's share of K-step c: kXA x values, 16 W values
+  // per step: x tile 64 x 32 (one float4 per thread), W tile 512 x 32 (eight float4 per thread);
+  // float4 f of the tile is (row f >> 3, k 4 (f & 7))
+  float4 sa, sb[8];
+  auto ld4 = [&](const float* row, int k) -> float4 {  // row[k .. k+3], zero past K
+    if constexpr (kVec) {
+      return k < K ? *reinterpret_cast<const float4*>(row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      return make_float4(k < K ? row[k] : 0.f, k + 1 < K ? row[k + 1] : 0.f, k + 2 < K ? row[k + 2] : 0.f,
+                         k + 3 < K ? row[k + 3] : 0.f);
+    }
+  };
+  auto load = [&](int c) {
     const int k0 = c * kMlpKC;
-#pragma unroll
-    for (int i = 0; i < kXA; ++i) {
-      const int idx = t + kNT * i, row = idx >> 4, kk = idx & 15;
-      const bool ok = r0 + row < R && k0 + kk < K;
-      sa[i] = ok ? x[(r0 + row) * x_ld + k0 + kk] : 0.0f;
+    {
+      const int row = t >> 3, k = k0 + 4 * (t & 7);
+      const int64_t rr = r0 + row < R ? r0 + row : R - 1;  // rows >= R: loaded, never stored
+      sa = ld4(x + rr * x_ld, k);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int idx = t + kNT * i, col = idx >> 4, kk = idx & 15;
-      sb[i] = (k0 + kk < K && (kLN || col < N)) ? w[(int64_t)col * w_ld + k0 + kk] : 0.0f;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < kXA; ++i) {
-      const int idx = t + kNT * i;
-      As[buf][(idx >> 4) * kMlpLd + (idx & 15)] = sa[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int idx = t + kNT * i;
-      Bs[buf][(idx >> 4) * kMlpLd + (idx & 15)] = sb[i];
+    for (int i = 0; i < 8; ++i) {
+      const int f = t + 512 * i, col = f >> 3, k = k0 + 4 * (f & 7);
+      sb[i] = ld4(w + (int64_t)col * w_ld, k);
     }
   };
-  f32x4_t acc[kRT][4];
+  auto store = [&]() {
+    *reinterpret_cast<float4*>(&As[(t >> 3) * kMlpLd + 4 * (t & 7)]) = sa;
 #pragma unroll
-  for (int i = 0; i < kRT; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int f = t + 512 * i;
+      *reinterpret_cast<float4*>(&Bs[(f >> 3) * kMlpLd + 4 * (f & 7)]) = sb[i];
+    }
+  };
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   load(0);
-  store(0);
-  __syncthreads();
   for (int c = 0; c < nc; ++c) {
-    const int buf = c & 1;
+    __syncthreads();  // every wave is done reading the previous step's stage
+    store();
+    __syncthreads();
     if (c + 1 < nc) load(c + 1);  // in flight under this step's MFMAs
-    float4 af[kRT], bf[4];
 #pragma unroll
-    for (int i = 0; i < kRT; ++i)
-      af[i] = *reinterpret_cast<const float4*>(&As[buf][(16 * i + l16) * kMlpLd + 4 * q]);
+    for (int h = 0; h < 2; ++h) {
+      float4 af[4], bf[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bf[j] = *reinterpret_cast<const float4*>(&Bs[buf][(64 * wv + 16 * j + l16) * kMlpLd + 4 * q]);
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *reinterpret_cast<const float4*>(&As[(16 * i + l16) * kMlpLd + 16 * h + 4 * q]);
+        bf[i] = *reinterpret_cast<const float4*>(&Bs[(64 * wv + 16 * i + l16) * kMlpLd + 16 * h + 4 * q]);
+      }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < 4; ++s) {
 #pragma unroll
-      for (int i = 0; i < kRT; ++i) {
-        const float a = s == 0 ? af[i].x : s == 1 ? af[i].y : s == 2 ? af[i].z : af[i].w;
+        for (int i = 0; i < 4; ++i) {
+          const float a = s == 0 ? af[i].x : s == 1 ? af[i].y : s == 2 ? af[i].z : af[i].w;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float b = s == 0 ? bf[j].x : s == 1 ? bf[j].y : s == 2 ? bf[j].z : bf[j].w;
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            const float b = s == 0 ? bf[j].x : s == 1 ? bf[j].y : s == 2 ? bf[j].z : bf[j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+          }
         }
       }
     }
-    if (c + 1 < nc) store(buf ^ 1);
-    __syncthreads();
   }
   // epilogue: acc[i][j][e] is row 16 i + 4 q + e, column 64 wv + 16 j + l16
-  if constexpr (!kLN) {
+  float cb[4], cw0[4], cw1[4], cg[4], cbt[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = 64 * wv + 16 * j + l16;
-      if (col >= N) continue;
-      const float cb = bias[col];
+  for (int j = 0; j < 4; ++j) {
+    const int col = 64 * wv + 16 * j + l16;
+    cb[j] = bias[col];
+    cw0[j] = e0 ? w[(int64_t)col * w_ld + K] : 0.0f;
+    cw1[j] = e1 ? w[(int64_t)col * w_ld + K + 1] : 0.0f;
+    cg[j] = gamma[col];
+    cbt[j] = beta[col];
+  }
+  float v[4][4][4];
 #pragma unroll
-      for (int i = 0; i < kRT; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t row = r0 + 16 * i + 4 * q + e;
-          if (row < R) y[row * y_ld + col] = acc[i][j][e] + cb;
-        }
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 16 * i + 4 * q + e;
+      const bool ok = row < R;
+      const float x0 = (e0 && ok) ? e0[row * e_ld] : 0.0f, x1 = (e1 && ok) ? e1[row * e_ld] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float h = acc[i][j][e] + cb[j];
+        if (e0) h += x0 * cw0[j];
+        if (e1) h += x1 * cw1[j];
+        v[i][j][e] = h;
+      }
     }
-  } else {
-    __shared__ float red[kNW][kRows];
-    __shared__ float stat[kRows];
-    float cb[4], cw0[4], cw1[4], cg[4], cbt[4];
+  // row means, then the biased variance about them (two passes, as accurate as torch's Welford)
+  auto row_reduce = [&](auto&& term) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = 64 * wv + 16 * j + l16;
-      cb[j] = bias[col];
-      cw0[j] = e0 ? w[(int64_t)col * w_ld + K] : 0.0f;
-      cw1[j] = e1 ? w[(int64_t)col * w_ld + K + 1] : 0.0f;
-      cg[j] = gamma[col];
-      cbt[j] = beta[col];
-    }
-    float v[kRT][4][4];
-#pragma unroll
-    for (int i = 0; i < kRT; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t row = r0 + 16 * i + 4 * q + e;
-        const bool ok = row < R;
-        const float x0 = (e0 && ok) ? e0[row * e_ld] : 0.0f, x1 = (e1 && ok) ? e1[row * e_ld] : 0.0f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float h = acc[i][j][e] + cb[j];
-          if (e0) h += x0 * cw0[j];
-          if (e1) h += x1 * cw1[j];
-          v[i][j][e] = h;
-        }
-      }
-    // row means, then the biased variance about them (two passes, as accurate as torch's Welford)
-    auto row_reduce = [&](auto&& term) {
-#pragma unroll
-      for (int i = 0; i < kRT; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float sum = 0.0f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) sum += term(i, j, e);
-#pragma unroll
-          for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the 16 lanes of one row
-          if (l16 == 0) red[wv][16 * i + 4 * q + e] = sum;
-        }
-      __syncthreads();
-      if (t < kRows) {
         float sum = 0.0f;
 #pragma unroll
-        for (int k = 0; k < kNW; ++k) sum += red[k][t];
-        stat[t] = sum * (1.0f / (float)kN);
+        for (int j = 0; j < 4; ++j) sum += term(i, j, e);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the 16 lanes of one row
+        if (l16 == 0) red[wv][16 * i + 4 * q + e] = sum;
       }
-      __syncthreads();
-    };
-    row_reduce([&](int i, int j, int e) { return v[i][j][e]; });
-    float mean[kRT][4];
+    __syncthreads();
+    if (t < kMlpRows) {
+      float sum = 0.0f;
 #pragma unroll
-    for (int i = 0; i < kRT; ++i)
+      for (int k = 0; k < 8; ++k) sum += red[k][t];
+      stat[t] = sum * (1.0f / (float)kMlpN);
+    }
+    __syncthreads();
+  };
+  row_reduce([&](int i, int j, int e) { return v[i][j][e]; });
+  float mean[4][4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mean[i][e] = stat[16 * i + 4 * q + e];
-    row_reduce([&](int i, int j, int e) {
-      const float d = v[i][j][e] - mean[i][e];
-      return d * d;
-    });
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < kRT; ++i)
+    for (int e = 0; e < 4; ++e) mean[i][e] = stat[16 * i + 4 * q + e];
+  row_reduce([&](int i, int j, int e) {
+    const float d = v[i][j][e] - mean[i][e];
+    return d * d;
+  });
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t row = r0 + 16 * i + 4 * q + e;
-        if (row >= R) continue;
-        const float rstd = 1.0f / sqrtf(stat[16 * i + 4 * q + e] + eps);
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float o = (v[i][j][e] - mean[i][e]) * rstd * cg[j] + cbt[j];
-          o = o >= 0.0f ? o : o * slope;
-          y[row * y_ld + 64 * wv + 16 * j + l16] = o;
-        }
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 16 * i + 4 * q + e;
+      if (row >= R) continue;
+      const float rstd = 1.0f / sqrtf(stat[16 * i + 4 * q + e] + eps);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o = (v[i][j][e] - mean[i][e]) * rstd * cg[j] + cbt[j];
+        o = o >= 0.0f ? o : o * slope;
+        y[row * y_ld + 64 * wv + 16 * j + l16] = o;
       }
-  }
+    }
 }
-
-constexpr int kMlpNW = 8, kMlpRT = 4;    // MLP block: 512 columns x 64 rows per workgroup
-constexpr int kLinNW = 3, kLinRT = 3;    // plain Linear: <= 192 columns x 48 rows per workgroup
 
 }  // namespace
 }  // namespace ddsp
@@ -490,26 +476,18 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
   const int64_t extra = e1 ? 2 : e0 ? 1 : 0;
   if (!x || !y || x_ld < in_features || w_ld < in_features + extra || y_ld < out_features || (extra && e_ld < 1))
     return DDSP_HIP_EINVAL;
-  constexpr int kRows = 16 * kMlpRT;
-  if (out_features != 64 * kMlpNW || in_features > INT32_MAX || (rows + kRows - 1) / kRows > INT32_MAX)
+  if (out_features != kMlpN || in_features > INT32_MAX || (rows + kMlpRows - 1) / kMlpRows > INT32_MAX)
     return DDSP_HIP_ERANGE;  // callers keep the GEMM + layer_norm_leaky_relu route
-  hipLaunchKernelGGL((mfma_rows_kernel<kMlpNW, kMlpRT, true>), dim3((unsigned)((rows + kRows - 1) / kRows)),
-                     dim3(64 * kMlpNW), 0, reinterpret_cast<hipStream_t>(stream), x, x_ld, (int)in_features, w, w_ld,
-                     bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows, (int)out_features);
-  return launch_status();
-}
-
-int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
-                    const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream) {
-  if (rows < 0 || in_features < 1 || out_features < 1 || !w || !bias) return DDSP_HIP_EINVAL;
-  if (rows == 0) return DDSP_HIP_OK;
-  if (!x || !y || x_ld < in_features || w_ld < in_features || y_ld < out_features) return DDSP_HIP_EINVAL;
-  constexpr int kRows = 16 * kLinRT;
-  if (out_features > 64 * kLinNW || in_features > INT32_MAX || (rows + kRows - 1) / kRows > INT32_MAX)
-    return DDSP_HIP_ERANGE;  // callers keep their GEMM
-  hipLaunchKernelGGL((mfma_rows_kernel<kLinNW, kLinRT, false>), dim3((unsigned)((rows + kRows - 1) / kRows)),
-                     dim3(64 * kLinNW), 0, reinterpret_cast<hipStream_t>(stream), x, x_ld, (int)in_features, w, w_ld,
-                     bias, nullptr, nullptr, 0, nullptr, nullptr, 0.0f, 0.0f, y, y_ld, rows, (int)out_features);
+  const bool vec = in_features % 4 == 0 && x_ld % 4 == 0 && w_ld % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) == 0;
+  const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (vec)
+    hipLaunchKernelGGL(mlp_block_kernel<true>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0,
+                       e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  else
+    hipLaunchKernelGGL(mlp_block_kernel<false>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0,
+                       e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows);
   return launch_status();
 }
 

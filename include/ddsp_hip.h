@@ -238,12 +238,6 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
                        const float* bias, const float* e0, const float* e1, int64_t e_ld, const float* gamma,
                        const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                        int64_t out_features, void* stream);
-/* y[r, :] = x[r, :in] W^T + bias for out_features <= 192 on the fp32 matrix cores: the decoder's
- * harmonic and noise projections (decoder.py:107-108, nn.Linear(hidden, n_harmonic + 1) and
- * nn.Linear(hidden, n_bands)) as ONE Linear over their stacked weights (166 outputs at config 2).
- * W [out_features, w_ld], y [rows, y_ld].  DDSP_HIP_ERANGE above 192 outputs (caller's GEMM). */
-int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
-                    const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream);
 int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1, const float* b1, const float* gamma,
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);

@@ -95,16 +95,3 @@ def test_mlp_forward_extras_match_cat(dd):
     with torch.no_grad():
         assert dd.core.mlp_block(gru_out, big[0], big[1], big[2]) is None
 
-
-@pytest.mark.parametrize("rows,n_out,k", [(12800, 166, 512), (47, 166, 512), (49, 101, 32), (1, 192, 17)])
-def test_linear_kernel(dd, rows, n_out, k):
-    """core.linear (the decoder's stacked projections on the matrix cores) against torch's Linear:
-    row counts around the 48-row workgroup tile, output counts inside the 192-column tile."""
-    torch.manual_seed(rows + n_out)
-    w = torch.randn(n_out, k, device="cuda") / k ** 0.5
-    b = torch.randn(n_out, device="cuda")
-    x = torch.randn(rows, k, device="cuda")
-    with torch.no_grad():
-        y = dd.core.linear(x, w, b)
-        torch.testing.assert_close(y, torch.nn.functional.linear(x, w, b), rtol=1e-5, atol=1e-5)
-        assert dd.core.linear(x, torch.randn(193, k, device="cuda"), torch.randn(193, device="cuda")) is None
