@@ -533,13 +533,28 @@ def gru(x, gru_module, h0=None):
     B, T, _ = x.shape
     H = g.hidden_size
     w_ih, w_hh, b_ih, b_hh = params
-    xp = torch.addmm(b_ih, x.reshape(B * T, -1), w_ih.t()).view(B, T, 3 * H)
     out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
     h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
     h0c = _c(h0.reshape(B, H)) if h0 is not None else None
-    _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
-              _lib.ptr(h_last), None, B, T, H, _lib.stream_of(out))
+    gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, None)
     return out, h_last
+
+
+def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates):
+    """The layer's forward on the device: ddsp_hip_gru_layer_forward (each step's input projection
+    inside its launch) where built (I = 1024, H = 512: the decoder's), else the input projection as
+    one GEMM + ddsp_hip_gru_forward."""
+    B, T, I = x.shape
+    H = w_hh.shape[1]
+    xc = _c(x)
+    st = _lib.call("gru_layer_forward", _lib.ptr(xc), _lib.ptr(_c(w_ih)), _lib.ptr(_c(b_ih)), _lib.ptr(_c(w_hh)),
+                   _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out), _lib.ptr(h_last), _lib.ptr(gates), B, T, I, H,
+                   _lib.stream_of(out), allow=(ERANGE,))
+    if st != ERANGE:
+        return
+    xp = torch.addmm(b_ih, xc.reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
+    _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
+              _lib.ptr(h_last), _lib.ptr(gates), B, T, H, _lib.stream_of(out))
 
 
 def mlp_block(x, linear, norm, act, out=None, extras=()):

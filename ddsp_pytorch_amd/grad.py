@@ -414,13 +414,11 @@ class GRUFn(_F):
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0):
         B, T, I = x.shape
         H = w_hh.shape[1]
-        xp = torch.addmm(b_ih, x.reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
         out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
         h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
         gates = torch.empty(4, B, T, H, dtype=torch.float32, device=x.device)
         h0c = core._c(h0.reshape(B, H)) if h0 is not None else None
-        _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(core._c(w_hh)), _lib.ptr(core._c(b_hh)), _lib.ptr(h0c),
-                  _lib.ptr(out), _lib.ptr(h_last), _lib.ptr(gates), B, T, H, _lib.stream_of(out))
+        core.gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates)
         ctx.save_for_backward(x, w_ih, w_hh, out, gates, h0c if h0c is not None else torch.empty(0))
         ctx.has_h0 = h0 is not None
         ctx.h0_shape = h0.shape if h0 is not None else None
