@@ -542,7 +542,7 @@ def gru(x, gru_module, h0=None):
 
 def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates):
     """The layer's forward on the device: ddsp_hip_gru_layer_forward (each step's input projection
-    inside its launch) where built (I = 1024, H = 512: the decoder's), else the input projection as
+    inside its launch) where built (H = 512, I = 1024 or 1536: the decoders'), else the input projection as
     one GEMM + ddsp_hip_gru_forward."""
     B, T, I = x.shape
     H = w_hh.shape[1]

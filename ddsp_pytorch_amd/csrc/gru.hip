@@ -717,8 +717,11 @@ int ddsp_hip_gru_layer_forward(const float* x, const float* w_ih, const float* b
   if (batch < 0 || steps < 0 || hidden < 1 || input_size < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!x || !w_ih || !b_ih || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
-  if (hidden != 512 || input_size != 1024) return DDSP_HIP_ERANGE;  // the caller's GEMM + ddsp_hip_gru_forward
-  return gru_forward_mfma<512, 1024>(x, w_ih, b_ih, w_hh, b_hh, h0, out, h_last, gates, batch, steps, stream);
+  if (hidden != 512 || (input_size != 1024 && input_size != 1536))
+    return DDSP_HIP_ERANGE;  // the caller's GEMM + ddsp_hip_gru_forward
+  if (input_size == 1024)    // DDSPDecoder's GRU(2 hidden, hidden)
+    return gru_forward_mfma<512, 1024>(x, w_ih, b_ih, w_hh, b_hh, h0, out, h_last, gates, batch, steps, stream);
+  return gru_forward_mfma<512, 1536>(x, w_ih, b_ih, w_hh, b_hh, h0, out, h_last, gates, batch, steps, stream);  // + z
 }
 
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,

@@ -257,8 +257,8 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
 /* The whole layer (torch.nn.GRU forward, decoder.py:33-68: GRU(2 * hidden, hidden)): x [B,T,I]
  * contiguous, W_ih [3H,I], b_ih [3H]; each step's input projection is computed inside that step's
  * launch (no [B,T,3H] projection buffer, no GEMM before the recurrence).  Other arguments as
- * ddsp_hip_gru_forward.  Built for I = 1024, H = 512 (DDSP_HIP_ERANGE otherwise: the caller's
- * GEMM + ddsp_hip_gru_forward). */
+ * ddsp_hip_gru_forward.  Built for H = 512 with I = 1024 (DDSPDecoder) or 1536 (with the z input,
+ * DDSPAutoencoder's decoder); DDSP_HIP_ERANGE otherwise (the caller's GEMM + ddsp_hip_gru_forward). */
 int ddsp_hip_gru_layer_forward(const float* x, const float* w_ih, const float* b_ih, const float* w_hh, const float* b_hh,
                                const float* h0, float* out, float* h_last, float* gates, int64_t batch, int64_t steps,
                                int64_t input_size, int64_t hidden, void* stream);

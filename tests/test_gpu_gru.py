@@ -24,7 +24,8 @@ def relerr(a, b):
 
 @pytest.mark.parametrize("B,T,I,H,with_h0", [(64, 200, 1024, 512, False), (1, 4, 1024, 512, True),
                                              (3, 17, 32, 64, True), (40, 9, 96, 128, False),
-                                             (20, 7, 64, 512, True), (20, 1, 64, 512, False)])
+                                             (20, 7, 1536, 512, True), (20, 1, 1024, 512, False),
+                                             (5, 3, 64, 512, True)])
 def test_gru_forward(dd, B, T, I, H, with_h0):
     torch.manual_seed(B * T + H)
     g = torch.nn.GRU(I, H, batch_first=True)
@@ -65,7 +66,7 @@ def test_decoder_gru_inference_and_training_paths_agree(dd):
 
 
 @pytest.mark.parametrize("B,T,I,H,with_h0", [(64, 50, 1024, 512, False), (3, 17, 32, 64, True),
-                                             (40, 9, 96, 128, True), (20, 6, 64, 512, True)])
+                                             (40, 9, 96, 128, True), (20, 6, 1024, 512, True)])
 def test_gru_backward(dd, B, T, I, H, with_h0):
     """BPTT on the step kernels vs torch's GRU autograd on the CPU: every gradient."""
     torch.manual_seed(B + T + H)
