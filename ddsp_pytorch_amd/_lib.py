@@ -130,10 +130,18 @@ def load():
     return _lib
 
 
+ERANGE = 5  # DDSP_HIP_ERANGE
+
+
 def call(name, *args, allow=()):
-    """Invoke ddsp_hip_<name>; map a non-zero status (other than those in `allow`) to RuntimeError."""
+    """Invoke ddsp_hip_<name>; map a non-zero status (other than those in `allow`) to RuntimeError.
+    An A/B build of an older revision (DDSP_HIP_LIB) that lacks an entry point whose caller has a
+    fallback (ERANGE allowed) answers ERANGE, so that the caller's fallback runs."""
     lib = load()
-    st = getattr(lib, "ddsp_hip_" + name)(*args)
+    fn = getattr(lib, "ddsp_hip_" + name, None)
+    if fn is None and ERANGE in allow and "DDSP_HIP_LIB" in os.environ:
+        return ERANGE
+    st = fn(*args)
     if st in allow:
         return st
     if st != 0:
