@@ -541,18 +541,12 @@ def gru(x, gru_module, h0=None):
 
 
 def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates):
-    """The layer's forward on the device: ddsp_hip_gru_layer_forward (each step's input projection
-    inside its launch) where built (H = 512, I = 1024 or 1536: the decoders'), else the input projection as
-    one GEMM + ddsp_hip_gru_forward."""
+    """The layer's forward on the device: the input projection for every step as one GEMM, then the
+    recurrence on ddsp_hip_gru_forward's step kernels (a form with each step's projection inside the
+    step launch measured slower: 13.3 vs 7.4-7.8 us per step)."""
     B, T, I = x.shape
     H = w_hh.shape[1]
-    xc = _c(x)
-    st = _lib.call("gru_layer_forward", _lib.ptr(xc), _lib.ptr(_c(w_ih)), _lib.ptr(_c(b_ih)), _lib.ptr(_c(w_hh)),
-                   _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out), _lib.ptr(h_last), _lib.ptr(gates), B, T, I, H,
-                   _lib.stream_of(out), allow=(ERANGE,))
-    if st != ERANGE:
-        return
-    xp = torch.addmm(b_ih, xc.reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
+    xp = torch.addmm(b_ih, _c(x).reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
     _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
               _lib.ptr(h_last), _lib.ptr(gates), B, T, H, _lib.stream_of(out))
 

@@ -246,7 +246,8 @@ __global__ void __launch_bounds__(256) ln_leaky_kernel(const float* __restrict__
 // double-buffered LDS stage left the loads exposed: 103 us per config-2 block, against 55 us of
 // MFMA issue).  Within a step lane l supplies k = 16 h + 4 (l >> 4) + s at sub-step (h, s) for both
 // operands (one ds_read_b128 per operand tile per half), so every product pairs x[r][k] with W[c][k].
-// kVec: 16-byte row loads (x and W rows 16-B aligned, K % 4 == 0), else scalar loads.  e0/e1
+// kVec: 4 = 16-byte loads (x and W rows 16-B aligned, K % 4 == 0); 2 = 8-byte loads (rows 8-B aligned,
+// K % 4 == 0: the out_mlp's W, 514 floats a row); 1 = scalar loads.  e0/e1
 // (optional): per-row scalars with weight columns K and K + 1 — the decoder's out_mlp input
 // [gru_out, f0, loudness] (decoder.py:68) without materialising the concatenation.
 constexpr int kMlpN = 512;          // output features (8 waves x 64)
@@ -255,7 +256,7 @@ constexpr int kMlpKC = 32;          // K per LDS stage
 constexpr int kMlpLd = kMlpKC + 4;  // LDS row stride (floats): 16-B aligned rows, banks spread
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <bool kVec>
+template <int kVec>
 __global__ void __launch_bounds__(512) mlp_block_kernel(
     const float* __restrict__ x, int64_t x_ld, int K, const float* __restrict__ w, int64_t w_ld,
     const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
@@ -273,8 +274,12 @@ __global__ void __launch_bounds__(512) mlp_block_kernel(
   // float4 f of the tile is (row f >> 3, k 4 (f & 7))
   float4 sa, sb[8];
   auto ld4 = [&](const float* row, int k) -> float4 {  // row[k .. k+3], zero past K
-    if constexpr (kVec) {
+    if constexpr (kVec == 4) {
       return k < K ? *reinterpret_cast<const float4*>(row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if constexpr (kVec == 2) {
+      if (k >= K) return make_float4(0.f, 0.f, 0.f, 0.f);
+      const float2 a = *reinterpret_cast<const float2*>(row + k), b = *reinterpret_cast<const float2*>(row + k + 2);
+      return make_float4(a.x, a.y, b.x, b.y);
     } else {
       return make_float4(k < K ? row[k] : 0.f, k + 1 < K ? row[k + 1] : 0.f, k + 2 < K ? row[k + 2] : 0.f,
                          k + 3 < K ? row[k + 3] : 0.f);
@@ -478,16 +483,20 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
     return DDSP_HIP_EINVAL;
   if (out_features != kMlpN || in_features > INT32_MAX || (rows + kMlpRows - 1) / kMlpRows > INT32_MAX)
     return DDSP_HIP_ERANGE;  // callers keep the GEMM + layer_norm_leaky_relu route
-  const bool vec = in_features % 4 == 0 && x_ld % 4 == 0 && w_ld % 4 == 0 &&
-                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) == 0;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
+  const int vec = in_features % 4 ? 1 : (x_ld % 4 == 0 && w_ld % 4 == 0 && (al & 15) == 0) ? 4
+                                      : (x_ld % 2 == 0 && w_ld % 2 == 0 && (al & 7) == 0) ? 2 : 1;
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (vec)
-    hipLaunchKernelGGL(mlp_block_kernel<true>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0,
-                       e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  if (vec == 4)
+    hipLaunchKernelGGL(mlp_block_kernel<4>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
+                       e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  else if (vec == 2)
+    hipLaunchKernelGGL(mlp_block_kernel<2>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
+                       e_ld, gamma, beta, eps, slope, y, y_ld, rows);
   else
-    hipLaunchKernelGGL(mlp_block_kernel<false>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0,
-                       e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+    hipLaunchKernelGGL(mlp_block_kernel<1>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
+                       e_ld, gamma, beta, eps, slope, y, y_ld, rows);
   return launch_status();
 }
 

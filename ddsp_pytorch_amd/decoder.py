@@ -211,8 +211,6 @@ def decoder_synthesize(self, hidden, f0):
     gfx950 kernels).  Works on this package's DDSPDecoder and, through install(), on the reference's.
     Returns (signal, harmonic, noise, harmonic_ctrls, noise_ctrls)."""
     hs, ns = self.harmonic_synth, self.noise_synth
-    if self.has_reverb:  # an IR rebuild due for this forward (new parameters) runs beside the synthesis
-        Reverb.prefetch(self.reverb, f0.shape[1] * int(hs.block_size))
     param, mags = decoder_projections(self, hidden)
     H, NB, bs = param.shape[-1] - 1, mags.shape[-1], int(hs.block_size)
     fused = (param.is_cuda and int(ns.block_size) == bs and param.shape[0] <= 65535

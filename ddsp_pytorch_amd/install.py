@@ -16,7 +16,7 @@ LOSS_FUNCTIONS = ("multiscale_fft", "safe_log")
 METHODS = {
     "HarmonicSynth": ("get_controls", "forward"),
     "FilteredNoise": ("get_controls", "forward", "draw_noise"),
-    "Reverb": ("build_impulse", "forward", "_spectrum", "_spec_cache_key", "prefetch"),
+    "Reverb": ("build_impulse", "forward", "_spectrum", "_spec_cache_key"),
 }
 
 

@@ -45,7 +45,6 @@ class Reverb(nn.Module):
         """Drop the cached IR spectrum (rebuilt on the next forward)."""
         self._spec_key = None
         self._spec = None
-        self._spec_pending = None
 
     def build_impulse(self):
         """modules.py:21-26 -> [1, length, 1]."""
@@ -55,48 +54,13 @@ class Reverb(nn.Module):
         return (n_samples, self.noise.device, self.noise.data_ptr(), self.noise._version,
                 self.decay._version, self.wet._version, self.decay.data_ptr(), self.wet.data_ptr())
 
-    def prefetch(self, n_samples):
-        """Start the IR rebuild that the next forward over n_samples needs — build_impulse and its
-        partition spectra (modules.py:21-26, 30-33) — on a side stream, so that it runs beside what the
-        caller launches next (the synthesis, which it does not depend on).  The side stream first waits
-        for the caller's stream (the parameters' last writes, e.g. an optimizer step); the next
-        ``_spectrum`` call for the same parameters makes the caller's stream wait for it.  A no-op when
-        the cached spectrum is current or the module is on the CPU.  (A reference Reverb instance works
-        too: only getattr-guarded attributes are read.)"""
-        if not self.noise.is_cuda:
-            return
-        key = Reverb._spec_cache_key(self, n_samples)
-        if key == getattr(self, "_spec_key", None) and (getattr(self, "cache_spectrum", True) or
-                                                        getattr(self, "_spec_pending", None) is not None):
-            return
-        dev = self.noise.device
-        side = getattr(self, "_side_stream", None)
-        if side is None or side.device != dev:
-            side = torch.cuda.Stream(dev)
-            self._side_stream = side
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side), torch.no_grad():
-            spec = core.reverb_impulse_spectrum(self.noise, self.decay, self.wet, self.sample_rate, n_samples)
-            done = torch.cuda.Event()
-            done.record(side)
-        self._spec, self._spec_key, self._spec_pending = spec, key, done
-
     def _spectrum(self, n_samples):
         key = Reverb._spec_cache_key(self, n_samples)
-        pending = getattr(self, "_spec_pending", None)
-        if pending is not None and key == getattr(self, "_spec_key", None):  # prefetched for this forward
-            spec = getattr(self, "_spec")
-            cur = torch.cuda.current_stream(self.noise.device)
-            cur.wait_event(pending)
-            spec.record_stream(cur)  # allocated on the side stream, read on this one
-            self._spec_pending = None
-            return spec
         if key != getattr(self, "_spec_key", None) or not getattr(self, "cache_spectrum", True):
             with torch.no_grad():  # build_impulse (modules.py:21-26) and its spectra: one launch
                 self._spec = core.reverb_impulse_spectrum(self.noise, self.decay, self.wet, self.sample_rate,
                                                           n_samples)
             self._spec_key = key
-            self._spec_pending = None
         return self._spec
 
     def forward(self, x):

@@ -71,8 +71,6 @@ class SynthPath(nn.Module):
 
     @torch.no_grad()
     def forward(self, f0, param, mags, noise=None):
-        if self.reverb is not None:  # an IR rebuild due for this call runs beside the synthesis
-            self.reverb.prefetch(f0.shape[1] * self.block_size)
         signal = self.synthesize(f0, param, mags, noise)
         if self.reverb is not None:
             with self._t("reverb"):

@@ -254,14 +254,6 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
  * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace: *_workspace_size. */
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                          float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream);
-/* The whole layer (torch.nn.GRU forward, decoder.py:33-68: GRU(2 * hidden, hidden)): x [B,T,I]
- * contiguous, W_ih [3H,I], b_ih [3H]; each step's input projection is computed inside that step's
- * launch (no [B,T,3H] projection buffer, no GEMM before the recurrence).  Other arguments as
- * ddsp_hip_gru_forward.  Built for H = 512 with I = 1024 (DDSPDecoder) or 1536 (with the z input,
- * DDSPAutoencoder's decoder); DDSP_HIP_ERANGE otherwise (the caller's GEMM + ddsp_hip_gru_forward). */
-int ddsp_hip_gru_layer_forward(const float* x, const float* w_ih, const float* b_ih, const float* w_hh, const float* b_hh,
-                               const float* h0, float* out, float* h_last, float* gates, int64_t batch, int64_t steps,
-                               int64_t input_size, int64_t hidden, void* stream);
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden);
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,

@@ -43,10 +43,10 @@ def test_uncached_reverb_golden(dd, tag):
     assert rms(out.cpu().numpy(), ref) < 2e-6 * max(1.0, float(np.sqrt(np.mean(ref ** 2))))
 
 
-def test_prefetched_ir_rebuild(dd):
-    """SynthPath.forward starts a due IR rebuild on the reverb's side stream before the synthesis
-    (Reverb.prefetch): with the cache off (the reference's rebuild-every-forward) and after in-place
-    parameter updates (an optimizer step), every call equals the same step with the IR built inline."""
+def test_ir_rebuild_every_call_and_after_updates(dd):
+    """With the cache off (the reference's rebuild-every-forward) and after in-place parameter updates
+    (an optimizer step), every SynthPath call equals the same step with the IR built by the separate
+    build_impulse + reverb_spectrum calls."""
     from ddsp_pytorch_amd.synth import SynthPath, make_inputs
     B, F, H, NB, bs, sr = 4, 20, 30, 65, 512, 48000
     inp = make_inputs(B, F, H, NB, bs, seed=2, device="cuda", with_noise=True)
@@ -66,8 +66,7 @@ def test_prefetched_ir_rebuild(dd):
     syn.reverb.cache_spectrum = True
     for k in range(3):
         with torch.no_grad():
-            syn.reverb.decay.add_(0.5)    # version bump: the next forward rebuilds (prefetched)
+            syn.reverb.decay.add_(0.5)    # version bump: the next forward rebuilds
             syn.reverb.wet.sub_(0.1)
         out = syn(*args)
-        assert syn.reverb._spec_pending is None  # consumed by this forward
         assert torch.equal(out, inline())

@@ -1,6 +1,6 @@
 """Development experiment: the GRU at the decoder's config-2 shape (B=64, T=200, I=1024, H=512):
 the whole layer on ddsp_hip_gru_layer_forward (each step's input projection inside its launch,
-when the loaded library has it), the split route (one hipBLASLt GEMM for the projection +
+when the loaded library has it: round 4's r04n build), the split route (one hipBLASLt GEMM for the projection +
 ddsp_hip_gru_forward's step kernels), the GEMM alone, and MIOpen's nn.GRU.  Runs against any
 library revision loaded through DDSP_HIP_LIB (tools/ab_time.sh)."""
 import json, os, sys, time
