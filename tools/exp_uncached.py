@@ -1,10 +1,9 @@
-"""Development experiment: bench.py's step at config 2 with the reverb IR cached, rebuilt every call
-with Reverb.prefetch (the rebuild on a side stream beside the synthesis), and rebuilt every call in
-line (prefetch disabled), host-timed over 200 steps after warmup."""
+"""Development experiment: bench.py's step at config 2 with the reverb IR cached and rebuilt every call
+(Reverb.cache_spectrum = False), host-timed over 200 steps after warmup.  (Round 4's r04n run also timed
+a side-stream prefetch of the rebuild, since removed: profiles/r04n_uncached.log.)"""
 import json, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
-from ddsp_pytorch_amd.modules import Reverb
 from ddsp_pytorch_amd.synth import SynthPath, make_inputs
 
 dev = "cuda"
@@ -30,11 +29,7 @@ def t(reps=200):
 
 res = {"cached_ms": t()}
 syn.reverb.cache_spectrum = False
-res["uncached_prefetch_ms"] = t()
-pf = Reverb.prefetch
-Reverb.prefetch = lambda self, n: None
-res["uncached_inline_ms"] = t()
-Reverb.prefetch = pf
+res["uncached_ms"] = t()
 syn.reverb.cache_spectrum = True
 res["cached_again_ms"] = t()
 print(json.dumps(res), flush=True)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 end check on one box: GPU tests, smoke, the driver's bench command (twice), decoder timings,
-# default / config 4 / config 5 lines, rocprofv3 kernel stats + PMC traffic, PMC VALU of the fused
-# kernel, GRU step-kernel A/B.  Each GPU step has its own limit; the chain stops at the first failure.
+# uncached-IR step, default / config 4 / config 5 lines, rocprofv3 kernel stats + PMC traffic, PMC VALU
+# of the fused kernel.  Each GPU step has its own limit; the chain stops at the first failure.
 TAG=${1:-r04m}
 set -o pipefail
 export TMPDIR=/tmp
@@ -24,11 +24,8 @@ timeout -k 10 200 python3 tools/exp_decoder2.py net net_gemm outmlp outmlp_gemm 
 cat gpurun_out/dec_$TAG.log
 timeout -k 10 100 python3 tools/exp_gru.py > gpurun_out/gru_$TAG.log 2>&1 || exit 1
 cat gpurun_out/gru_$TAG.log
-echo "== gru A/B $(date +%T)"
-bash tools/ab_prof.sh gru step_kernel grunew grumfma || exit 1
-cp gpurun_out/ab_prof.log gpurun_out/ab_prof_fwd_$TAG.log; cat gpurun_out/ab_prof.log
-bash tools/ab_prof.sh gru_train bwd_step grunew grumfma || exit 1
-cp gpurun_out/ab_prof.log gpurun_out/ab_prof_bwd_$TAG.log; cat gpurun_out/ab_prof.log
+timeout -k 10 200 python3 tools/exp_uncached.py > gpurun_out/unc_$TAG.log 2>&1 || exit 1
+cat gpurun_out/unc_$TAG.log
 echo "== decoder profile $(date +%T)"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dec_$TAG -o t -- python3 tools/exp_decoder2.py outmlp outmlp_gemm fwd > gpurun_out/prof_dec_$TAG.log 2>&1 || exit 1
 echo "== bench default $(date +%T)"
