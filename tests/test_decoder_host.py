@@ -12,34 +12,42 @@ def _cat(m):
             torch.cat([m.harmonic_proj.bias, m.noise_proj.bias]).detach())
 
 
+def _sp(m):
+    """The shared buffer's live rows (it is zero-padded to a multiple of 64 outputs for the GEMM)."""
+    w, b = _shared_projection(m)
+    n = m.harmonic_proj.out_features + m.noise_proj.out_features
+    assert w.shape[0] % 64 == 0 and not w[n:].any() and not b[n:].any()
+    return w[:n], b[:n]
+
+
 def test_shared_projection_is_live():
     torch.manual_seed(0)
     m = dd.DDSPDecoder(32, 10, 9, 48000, 64, False)
-    w, b = _shared_projection(m)
+    w, b = _sp(m)
     assert torch.equal(w, _cat(m)[0]) and torch.equal(b, _cat(m)[1])
     # the parameters are views of the shared buffer: in-place writes through .data are seen
     m.harmonic_proj.weight.data.mul_(2.0)
-    w2, b2 = _shared_projection(m)
-    assert w2 is w and torch.equal(w2, _cat(m)[0])
+    w2, b2 = _sp(m)
+    assert w2.data_ptr() == w.data_ptr() and torch.equal(w2, _cat(m)[0])
     m.noise_proj.bias.data.copy_(torch.arange(9.0))
-    assert torch.equal(_shared_projection(m)[1], _cat(m)[1])
+    assert torch.equal(_sp(m)[1], _cat(m)[1])
     # load_state_dict copies into the parameters in place
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     sd["harmonic_proj.weight"].fill_(0.5)
     m.load_state_dict(sd)
-    assert torch.equal(_shared_projection(m)[0], _cat(m)[0])
+    assert torch.equal(_sp(m)[0], _cat(m)[0])
     # a replaced .data (or a fresh module) is re-shared with its current values
     m.noise_proj.weight.data = torch.randn(9, 32)
-    w3, _ = _shared_projection(m)
-    assert w3 is not w and torch.equal(w3, _cat(m)[0])
+    w3, _ = _sp(m)
+    assert w3.data_ptr() != w.data_ptr() and torch.equal(w3, _cat(m)[0])
     m.harmonic_proj = torch.nn.Linear(32, 11)
-    assert torch.equal(_shared_projection(m)[0], _cat(m)[0])
+    assert torch.equal(_sp(m)[0], _cat(m)[0])
     # an optimizer step updates the shared storage too
     opt = torch.optim.SGD(m.parameters(), lr=0.1)
     for p in m.parameters():
         p.grad = torch.ones_like(p)
     opt.step()
-    assert torch.equal(_shared_projection(m)[0], _cat(m)[0])
+    assert torch.equal(_sp(m)[0], _cat(m)[0])
 
 
 def test_synth_overridden():
