@@ -712,14 +712,17 @@ def main():
         # the reference rebuilds the impulse and its transform on every Reverb.forward
         # (modules.py:30-33); the module caches the spectrum between calls.  Same step with the
         # cache off: build_impulse + partition spectra + the rest, every call.
+        # timed at steady state over at least 200 steps (20 steps of a 0.2 ms step are a 4 ms window in
+        # which one host hiccup moves the mean by several per cent)
         syn.reverb.cache_spectrum = False
+        n_unc = max(args.steps, 200)
         for _ in range(5):
             step()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         tu = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(n_unc):
             step()
         torch.cuda.synchronize()
         tu = time.perf_counter() - tu
@@ -729,8 +732,8 @@ def main():
             tt = torch.tensor([tu], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             tu = float(tt.item())
-        result["uncached_ir"] = {"value": round(samples_per_step * args.steps / tu, 1), "unit": "samples/s",
-                                 "ms_per_step": round(tu / args.steps * 1e3, 4),
+        result["uncached_ir"] = {"value": round(samples_per_step * n_unc / tu, 1), "unit": "samples/s",
+                                 "ms_per_step": round(tu / n_unc * 1e3, 4), "steps_timed": n_unc,
                                  "note": "step with the reverb IR and its partition spectra rebuilt every call "
                                          "(Reverb.cache_spectrum = False), as the reference's Reverb.forward does"}
 
