@@ -70,9 +70,12 @@ SIGNATURES = {
     "ddsp_hip_reverb_spectrum": (_I, [_P, _I64, _I64, _P, _P]),
     "ddsp_hip_reverb_impulse_spectrum": (_I, [_P, _P, _P, _I64, _F, _I64, _P, _P]),
     "ddsp_hip_reverb_apply": (_I, [_P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_reverb_cache_bytes": (_SZ, [_I64, _I64]),
+    "ddsp_hip_reverb_forward": (_I, [_P, _P, _P, _P, _I64, _F, _I, _P, _SZ, _P, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_dense_rows": (_I, [_P, _I, _I64, _P]),
     "ddsp_hip_mlp_block": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _F, _F, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_layer_norm_leaky_relu": (_I, [_P, _I64, _P, _P, _P, _P, _F, _F, _P, _I64, _I64, _I64, _P]),
+    "ddsp_hip_projections": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _P]),
     "ddsp_hip_gru_forward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_gru_backward_workspace_size": (_SZ, [_I64, _I64]),
     "ddsp_hip_gru_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
@@ -138,8 +141,10 @@ def call(name, *args, allow=()):
     fallback (ERANGE allowed) answers ERANGE, so that the caller's fallback runs."""
     lib = load()
     fn = getattr(lib, "ddsp_hip_" + name, None)
-    if fn is None and ERANGE in allow and "DDSP_HIP_LIB" in os.environ:
-        return ERANGE
+    if fn is None:
+        if ERANGE in allow and "DDSP_HIP_LIB" in os.environ:
+            return ERANGE
+        raise RuntimeError(f"ddsp_hip: entry point ddsp_hip_{name} is missing from {LIB_PATH}")
     st = fn(*args)
     if st in allow:
         return st

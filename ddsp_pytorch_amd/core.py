@@ -26,7 +26,7 @@ __all__ = [
     "scale_function", "remove_above_nyquist", "upsample", "harmonic_synth",
     "amp_to_impulse_response", "fft_convolve", "phase", "harmonic_controls",
     "harmonic_synth_frames", "harmonic_synth_params", "synth_frames", "filtered_noise", "reverb_build_impulse", "reverb_spectrum_floats",
-    "reverb_spectrum", "reverb_impulse_spectrum", "reverb_apply", "set_noise_seed", "safe_log", "stft_magnitude", "multiscale_fft",
+    "reverb_spectrum", "reverb_impulse_spectrum", "reverb_apply", "reverb_forward", "reverb_cache_bytes", "set_noise_seed", "safe_log", "stft_magnitude", "multiscale_fft",
 ]
 
 
@@ -498,6 +498,33 @@ def reverb_impulse_spectrum(noise, decay, wet, sample_rate, n_samples):
     return spec
 
 
+def reverb_cache_bytes(n_samples, ir_length):
+    return int(_lib.query("reverb_cache_bytes", int(n_samples), int(ir_length)))
+
+
+def reverb_forward(x, noise, decay, wet, ir_length, sample_rate, cache, force=False, n_samples=None):
+    """modules.py:21-35 Reverb.forward over a device IR cache that the launch validates against the
+    parameters (ddsp_hip_reverb_forward) -> (out [B, T, 1], workspace, spectrum view of the cache).  With
+    x None only the cache is validated (for inputs of n_samples).  No autograd (grad.ReverbFn wraps it)."""
+    _dev(noise, decay, wet)
+    if x is not None:
+        _dev(x)
+        B, T = x.shape[0], x.shape[1]
+        xc = _c(x)
+    else:
+        B, T, xc = 0, int(n_samples), None
+    L = int(ir_length)
+    if cache.device != noise.device or cache.numel() < reverb_cache_bytes(T, L):
+        raise RuntimeError("reverb_forward: cache on another device or too small")
+    out = torch.empty(B, T, 1, dtype=torch.float32, device=noise.device) if B else None
+    ws = _workspace(_lib.query("reverb_workspace_size", B, T, L), noise.device) if B else None
+    _lib.call("reverb_forward", _lib.ptr(xc), _lib.ptr(_c(noise)), _lib.ptr(_c(decay)), _lib.ptr(_c(wet)), L,
+              float(sample_rate), int(bool(force)), _lib.ptr(cache), cache.numel(), _lib.ptr(out), B, T,
+              _lib.ptr(ws), ws.numel() if ws is not None else 0, _lib.stream_of(cache))
+    spec = cache[:4 * reverb_spectrum_floats(T, L)].view(torch.float32)
+    return out, ws, spec
+
+
 def reverb_apply(x, spectrum, ir_length):
     """modules.py:28-35 Reverb.forward given the cached IR spectrum: x [B, T, 1] -> [B, T, 1]."""
     _dev(x, spectrum)
@@ -579,6 +606,30 @@ def mlp_block(x, linear, norm, act, out=None, extras=()):
                    _lib.ptr(_c(norm.weight)), _lib.ptr(_c(norm.bias)), float(norm.eps), float(act.negative_slope),
                    _lib.ptr(out), int(y_ld), int(rows), n_out, _lib.stream_of(out), allow=(ERANGE,))
     return None if st == ERANGE else out
+
+
+def projections(x, lin1, lin2):
+    """decoder.py:106-117: (lin1(x), lin2(x)) — harmonic_proj and noise_proj — as ONE launch reading both
+    nn.Linear layers' own parameters (ddsp_hip_projections: fp32 matrix cores).  The two results are
+    column slices of one [..., n1 + n2 (rounded up to 4)] buffer, which the fused synthesis kernel reads
+    with that row stride.  Returns None where the kernel does not apply (the caller runs torch's
+    Linear layers); inference only."""
+    _dev(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+    n1, n2, K = lin1.out_features, lin2.out_features, x.shape[-1]
+    if lin1.in_features != K or lin2.in_features != K:
+        raise RuntimeError(f"projections: input features {K} vs {lin1.in_features} / {lin2.in_features}")
+    xc = _c(x)
+    lead = tuple(x.shape[:-1])
+    rows = xc.numel() // K if K else 0
+    ld = -(-(n1 + n2) // 4) * 4
+    y = torch.empty(*lead, ld, dtype=torch.float32, device=x.device)
+    w1, w2 = _c(lin1.weight), _c(lin2.weight)
+    st = _lib.call("projections", _lib.ptr(xc), K, K, _lib.ptr(w1), w1.stride(0), _lib.ptr(_c(lin1.bias)), n1,
+                   _lib.ptr(w2), w2.stride(0), _lib.ptr(_c(lin2.bias)), n2, _lib.ptr(y), ld, int(rows),
+                   _lib.stream_of(y), allow=(ERANGE,))
+    if st == ERANGE:
+        return None
+    return y[..., :n1], y[..., n1:n1 + n2]
 
 
 def layer_norm_leaky_relu(h, norm, act, out=None, w1=None, b1=None):

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 
 #include "common.h"
 
@@ -414,6 +415,127 @@ __global__ void __launch_bounds__(512) mlp_block_kernel(
     }
 }
 
+// decoder.py:106-117, the two projections after the decoder network as ONE launch that reads both
+// nn.Linear layers' own parameters: y[r][c] = b[c] + sum_k x[r][k] W[c][k], (W, b) = harmonic_proj's
+// for c < n1, noise_proj's for n1 <= c < n1 + n2.  Same staging as mlp_block_kernel (exact fp32
+// v_mfma_f32_16x16x4_f32, x and W through one LDS stage of K = 32, the next stage's operands in
+// registers under the current stage's MFMAs).  A workgroup owns 64 rows and all NT 16-column tiles;
+// wave w computes row tile w & 3 against half w >> 2 of the column tiles (one A fragment shared by up
+// to 8 B tiles per LDS read).  Columns past n1 + n2 are zero weights, never stored.
+constexpr int kProjRows = 64;
+constexpr int kProjKC = 32;
+constexpr int kProjLd = kProjKC + 4;
+constexpr int kProjMaxTiles = 14;  // 224 columns (15 and 16 tiles spilled)
+
+template <int NT>
+__global__ void __launch_bounds__(512) projections_kernel(
+    const float* __restrict__ x, int64_t x_ld, int K, const float* __restrict__ w1, int64_t w1_ld,
+    const float* __restrict__ b1, int n1, const float* __restrict__ w2, int64_t w2_ld,
+    const float* __restrict__ b2, int n2, float* __restrict__ y, int64_t y_ld, int64_t R) {
+  constexpr int NA = (NT + 1) / 2;               // column tiles per wave (an odd NT pads one zero tile)
+  constexpr int NC = 2 * NA * 16;                // columns staged
+  constexpr int NBL = (NC * 8 + 511) / 512;      // W float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) float As[kProjRows * kProjLd];
+  __shared__ __attribute__((aligned(16))) float Bs[NC * kProjLd];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int rt = wv & 3, tile0 = (wv >> 2) * NA;
+  const int64_t r0 = (int64_t)blockIdx.x * kProjRows;
+  const int nc = (K + kProjKC - 1) / kProjKC, ncol = n1 + n2;
+  // every load is unconditional from a valid address (clamped row / column / k) and zeroed by a
+  // select past the matrix: no divergent branches around the loads
+  const int arow = t >> 3;
+  const float* xrow = x + (r0 + arow < R ? r0 + arow : R - 1) * x_ld;
+  const float* wr[NBL];
+  bool wok[NBL];
+#pragma unroll
+  for (int i = 0; i < NBL; ++i) {
+    const int col = (t + 512 * i) >> 3;
+    const int cc = col < ncol ? col : ncol - 1;
+    wr[i] = cc < n1 ? w1 + (int64_t)cc * w1_ld : w2 + (int64_t)(cc - n1) * w2_ld;
+    wok[i] = col < ncol;
+  }
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sa, sb[NBL];
+  auto load = [&](int c) {
+    const int k = c * kProjKC + 4 * (t & 7);
+    const int kk = k < K ? k : K - 4;
+    sa = *reinterpret_cast<const float4*>(xrow + kk);
+    if (k >= K) sa = z4;
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      sb[i] = *reinterpret_cast<const float4*>(wr[i] + kk);
+      if (!wok[i] || k >= K) sb[i] = z4;
+    }
+  };
+  auto store = [&]() {
+    *reinterpret_cast<float4*>(&As[arow * kProjLd + 4 * (t & 7)]) = sa;
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      const int f = t + 512 * i;
+      if (NBL * 512 == NC * 8 || f < NC * 8) *reinterpret_cast<float4*>(&Bs[(f >> 3) * kProjLd + 4 * (f & 7)]) = sb[i];
+    }
+  };
+  f32x4_t acc[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int c = 0; c < nc; ++c) {
+    __syncthreads();  // every wave is done reading the previous stage
+    store();
+    __syncthreads();
+    if (c + 1 < nc) load(c + 1);  // in flight under this stage's MFMAs
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 af = *reinterpret_cast<const float4*>(&As[(16 * rt + l16) * kProjLd + 16 * h + 4 * q]);
+      float4 bf[NA];
+#pragma unroll
+      for (int j = 0; j < NA; ++j)
+        bf[j] = *reinterpret_cast<const float4*>(&Bs[(16 * (tile0 + j) + l16) * kProjLd + 16 * h + 4 * q]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float a = s == 0 ? af.x : s == 1 ? af.y : s == 2 ? af.z : af.w;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          const float b = s == 0 ? bf[j].x : s == 1 ? bf[j].y : s == 2 ? bf[j].z : bf[j].w;
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // acc[j][e] is row 16 rt + 4 q + e, column 16 (tile0 + j) + l16
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int col = 16 * (tile0 + j) + l16;
+    if (col >= ncol) continue;
+    const float bias = col < n1 ? b1[col] : b2[col - n1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 16 * rt + 4 * q + e;
+      if (row < R) y[row * y_ld + col] = acc[j][e] + bias;
+    }
+  }
+}
+
+template <int NT>
+void launch_projections(dim3 grid, hipStream_t st, const float* x, int64_t x_ld, int K, const float* w1,
+                        int64_t w1_ld, const float* b1, int n1, const float* w2, int64_t w2_ld, const float* b2,
+                        int n2, float* y, int64_t y_ld, int64_t R) {
+  hipLaunchKernelGGL(projections_kernel<NT>, grid, dim3(512), 0, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2,
+                     n2, y, y_ld, R);
+}
+
+template <int... NTs>
+void dispatch_projections(int nt, std::integer_sequence<int, NTs...>, dim3 grid, hipStream_t st, const float* x,
+                          int64_t x_ld, int K, const float* w1, int64_t w1_ld, const float* b1, int n1,
+                          const float* w2, int64_t w2_ld, const float* b2, int n2, float* y, int64_t y_ld,
+                          int64_t R) {
+  ((nt == NTs + 1 ? launch_projections<NTs + 1>(grid, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2, n2, y, y_ld,
+                                                R)
+                  : void()),
+   ...);
+}
+
 }  // namespace
 }  // namespace ddsp
 
@@ -497,6 +619,26 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
   else
     hipLaunchKernelGGL(mlp_block_kernel<1>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
                        e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  return launch_status();
+}
+
+int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, const float* w1, int64_t w1_ld,
+                         const float* b1, int64_t n1, const float* w2, int64_t w2_ld, const float* b2, int64_t n2,
+                         float* y, int64_t y_ld, int64_t rows, void* stream) {
+  if (rows < 0 || in_features < 1 || n1 < 1 || n2 < 0 || !w1 || !b1 || (n2 > 0 && (!w2 || !b2)))
+    return DDSP_HIP_EINVAL;
+  if (rows == 0) return DDSP_HIP_OK;
+  if (!x || !y || x_ld < in_features || w1_ld < in_features || (n2 > 0 && w2_ld < in_features) || y_ld < n1 + n2)
+    return DDSP_HIP_EINVAL;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w1) |
+                       (n2 > 0 ? reinterpret_cast<uintptr_t>(w2) : 0);
+  if (n1 + n2 > 16 * kProjMaxTiles || in_features % 4 || in_features > INT32_MAX || (al & 15) || (x_ld & 3) || (w1_ld & 3) ||
+      (n2 > 0 && (w2_ld & 3)) || (rows + kProjRows - 1) / kProjRows > INT32_MAX)
+    return DDSP_HIP_ERANGE;  // callers keep torch's Linear
+  const int nt = (int)((n1 + n2 + 15) / 16);
+  const dim3 grid((unsigned)((rows + kProjRows - 1) / kProjRows));
+  dispatch_projections(nt, std::make_integer_sequence<int, kProjMaxTiles>{}, grid, reinterpret_cast<hipStream_t>(stream), x,
+                       x_ld, (int)in_features, w1, w1_ld, b1, (int)n1, w2, w2_ld, b2, (int)n2, y, y_ld, rows);
   return launch_status();
 }
 

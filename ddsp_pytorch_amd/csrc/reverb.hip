@@ -156,6 +156,23 @@ int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int
                      workspace, workspace_bytes, stream);
 }
 
+size_t ddsp_hip_reverb_cache_bytes(int64_t n_samples, int64_t ir_length) {
+  if (n_samples < 1 || ir_length < 1) return 0;
+  return upols_ir_cache_bytes(std::min(ir_length, n_samples));
+}
+
+int ddsp_hip_reverb_forward(const float* x, const float* noise, const float* decay, const float* wet,
+                            int64_t ir_length, float sample_rate, int force, void* cache, size_t cache_bytes,
+                            float* out, int64_t batch, int64_t n_samples, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  if (batch < 0 || n_samples < 1 || ir_length < 1 || !noise || !decay || !wet || !(sample_rate > 0))
+    return DDSP_HIP_EINVAL;
+  if (batch > 0 && (!x || !out)) return DDSP_HIP_EINVAL;
+  if (!cache || cache_bytes < ddsp_hip_reverb_cache_bytes(n_samples, ir_length)) return DDSP_HIP_EWORKSPACE;
+  return upols_reverb_cached(x, batch, n_samples, noise, decay, wet, std::min(ir_length, n_samples), sample_rate,
+                             force, cache, out, workspace, workspace_bytes, stream);
+}
+
 int ddsp_hip_reverb_apply_transposed(const float* grad, const float* spectrum, float* grad_x, int64_t batch,
                                      int64_t n_samples, int64_t ir_length, void* workspace,
                                      size_t workspace_bytes, void* stream) {

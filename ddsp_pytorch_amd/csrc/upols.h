@@ -29,6 +29,14 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
 // rows ([npairs][nb][kN], e.g. written by the fused synthesis kernel), Y = workspace of the same size.
 int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* spectrum, int64_t klen,
                         bool per_row_kernel, float* y, float2* Y, void* stream, bool reverse = false);
+// The reverb with its IR spectrum cached on the device and validated against (noise, decay, wet, sr)
+// on every call, per kernel window, in the forward transform's launch (force: rebuild every window).
+// cache: upols_ir_cache_bytes(klen), zero-filled when new; its first upols_spectrum_floats(1, klen)
+// floats are the spectrum.  rows == 0: validate / rebuild the cache only.
+size_t upols_ir_cache_bytes(int64_t klen);
+int upols_reverb_cached(const float* x, int64_t rows, int64_t n, const float* noise, const float* decay,
+                        const float* wet, int64_t klen, float sr, int force, void* cache, float* y, void* ws,
+                        size_t ws_bytes, void* stream);
 // bytes of the input spectra X that upols_apply leaves at the start of its workspace (pairing)
 size_t upols_spectra_bytes(int64_t rows, int64_t n);
 // Backward of upols_apply with a kernel shared by all rows (pairing): dx[rows, n] (nullable) and

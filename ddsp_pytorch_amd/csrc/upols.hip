@@ -94,12 +94,10 @@ __device__ __forceinline__ void pair_rows(int pair, int rows, int pairing, int& 
 //   off = -1, zero_half = 1: FFT([0, z_b]), the adjoint of the inverse transform's "keep the
 //   second half" (backward).  reverse: z read time-reversed (z'[s] = z[T-1-s], the transposed
 //   convolution of the input gradient).
-__global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
-                                                            int64_t T, int rows, int pairing, int nb,
-                                                            int off, int zero_half, int reverse,
-                                                            float2* __restrict__ X) {
-  __shared__ float2 lds[kPad];
-  const int b = blockIdx.x, pair = blockIdx.y, j = threadIdx.x;
+__device__ __forceinline__ void forward_block(const float* __restrict__ x, int64_t ld, int64_t T, int rows,
+                                              int pairing, int nb, int off, int zero_half, int reverse,
+                                              float2* __restrict__ X, int b, int pair, float2* lds) {
+  const int j = threadIdx.x;
   int ra, rb;
   pair_rows(pair, rows, pairing, ra, rb);
   const float* xa = x + (int64_t)ra * ld;
@@ -117,6 +115,93 @@ __global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restr
   float2* out = X + ((int64_t)pair * nb + b) * kN;
 #pragma unroll
   for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+}
+
+__global__ void __launch_bounds__(kNT) upols_forward_kernel(const float* __restrict__ x, int64_t ld,
+                                                            int64_t T, int rows, int pairing, int nb,
+                                                            int off, int zero_half, int reverse,
+                                                            float2* __restrict__ X) {
+  __shared__ float2 lds[kPad];
+  forward_block(x, ld, T, rows, pairing, nb, off, zero_half, reverse, X, blockIdx.x, blockIdx.y, lds);
+}
+
+// The reverb's IR spectrum cached on the device and validated there on every call (Reverb.forward,
+// modules.py:21-35, rebuilds it every call; a host-side cache keyed on parameter versions misses
+// writes through .data).  Per kernel window q the cache keeps the spectrum G_q and a snapshot of the
+// exact inputs it was built from — the noise taps of the window [(q-1)P, (q+1)P) ∩ [0, klen) bit for
+// bit, decay, wet, the sample rate and klen + 1 (0 in a zero-filled cache: nothing valid yet).  The
+// window's workgroup compares them with the current parameters and rebuilds G_q (the arithmetic of
+// upols_impulse_spectrum_kernel, bit for bit) only when one differs or `force` is set.  Each
+// window's snapshot is its own (windows overlap by P taps), so no two workgroups write one word.
+constexpr int kSnapWords = 2 * kP + 4;
+
+__device__ __forceinline__ void ir_window(const float* __restrict__ noise, const float* __restrict__ decay,
+                                          const float* __restrict__ wet, int64_t klen, float sr, int force, int q,
+                                          float2* __restrict__ Hs, uint32_t* __restrict__ snap, float2* lds) {
+  const int j = threadIdx.x;
+  uint32_t* sq = snap + (int64_t)q * kSnapWords;
+  float nv[16];
+  bool diff = false;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = (int64_t)(q - 1) * kP + j + 256 * r;
+    const bool in = s >= 0 && s < klen;
+    nv[r] = in ? noise[s] : 0.0f;
+    diff |= in && __float_as_uint(nv[r]) != sq[j + 256 * r];
+  }
+  const float dec = decay[0], wt = wet[0];
+  if (j == 0)
+    diff |= sq[2 * kP] != __float_as_uint(dec) || sq[2 * kP + 1] != __float_as_uint(wt) ||
+            sq[2 * kP + 2] != __float_as_uint(sr) || sq[2 * kP + 3] != (uint32_t)(klen + 1);
+  if (!__syncthreads_or(diff || force)) return;  // the cached G_q is this window's spectrum
+  const float d = -dec;
+  const float sp = d > 20.0f ? d : log1pf(expf(d));  // softplus(-decay), torch's threshold 20
+  const float neg = -sp;
+  const float w = 1.0f / (1.0f + expf(-wt));
+  const float inv_n = 1.0f / (float)kN;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = (int64_t)(q - 1) * kP + j + 256 * r;
+    float h = 0.0f;
+    if (s >= 0 && s < klen) {
+      const float t = (float)s / sr;
+      const float env = expf((neg * t) * 500.0f);
+      h = s == 0 ? 1.0f : (nv[r] * env) * w;
+    }
+    v[r] = make_float2(h * inv_n, 0.0f);
+  }
+  fft4096<false>(v, lds);
+  float2* out = Hs + (int64_t)q * kN;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[j + 256 * r] = v[r];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t s = (int64_t)(q - 1) * kP + j + 256 * r;
+    if (s >= 0 && s < klen) sq[j + 256 * r] = __float_as_uint(nv[r]);
+  }
+  if (j == 0) {
+    sq[2 * kP] = __float_as_uint(dec);
+    sq[2 * kP + 1] = __float_as_uint(wt);
+    sq[2 * kP + 2] = __float_as_uint(sr);
+    sq[2 * kP + 3] = (uint32_t)(klen + 1);
+  }
+}
+
+// The reverb's forward transform (Z_b = FFT([x_b, 0]), grid rows y < npairs) with the IR cache's
+// validation in the same launch (row y = npairs, x = window): the MAC that follows reads a spectrum
+// that is current, and no launch is added to the step.  npairs == 0: the validation alone.
+__global__ void __launch_bounds__(kNT) upols_forward_ir_kernel(
+    const float* __restrict__ x, int64_t T, int rows, int nb, float2* __restrict__ X, const float* __restrict__ noise,
+    const float* __restrict__ decay, const float* __restrict__ wet, int64_t klen, float sr, int force, int QG,
+    float2* __restrict__ Hs, uint32_t* __restrict__ snap) {
+  __shared__ float2 lds[kPad];
+  const int npairs = (int)gridDim.y - 1;
+  if ((int)blockIdx.y == npairs) {
+    if ((int)blockIdx.x < QG) ir_window(noise, decay, wet, klen, sr, force, blockIdx.x, Hs, snap, lds);
+  } else if ((int)blockIdx.x < nb) {
+    forward_block(x, T, T, rows, 1, nb, 0, 2, 0, X, blockIdx.x, blockIdx.y, lds);
+  }
 }
 
 // 8-byte load at byte offset voff of one spectrum row through a raw buffer descriptor (stride 0,
@@ -541,6 +626,30 @@ int upols_apply(const float* x, int64_t rows, int64_t n, const float* spectrum, 
   int st = launch_forward(x, n, rows, (int)pairing, nb, npairs, 0, 2, (int)reverse, X, stream);
   if (st) return st;
   return upols_apply_spectra(X, rows, n, spectrum, klen, per_row_kernel, y, Y, stream, reverse);
+}
+
+size_t upols_ir_cache_bytes(int64_t klen) {
+  const int64_t QG = upols_kernel_windows(klen);
+  return (size_t)QG * kN * sizeof(float2) + (size_t)QG * kSnapWords * sizeof(uint32_t);
+}
+
+int upols_reverb_cached(const float* x, int64_t rows, int64_t n, const float* noise, const float* decay,
+                        const float* wet, int64_t klen, float sr, int force, void* cache, float* y, void* ws,
+                        size_t ws_bytes, void* stream) {
+  const int64_t QG = upols_kernel_windows(klen);
+  const int64_t npairs = (rows + 1) / 2;
+  const int64_t nb = rows > 0 ? upols_blocks(n) : 0;
+  if (QG > 65535 || nb > 65535 || npairs > 65534) return DDSP_HIP_EINVAL;
+  if (rows > 0 && (!ws || ws_bytes < upols_workspace_bytes(rows, n, true))) return DDSP_HIP_EWORKSPACE;
+  float2* Hs = reinterpret_cast<float2*>(cache);
+  uint32_t* snap = reinterpret_cast<uint32_t*>(Hs + (size_t)QG * kN);
+  float2* X = reinterpret_cast<float2*>(ws);
+  hipLaunchKernelGGL(upols_forward_ir_kernel, dim3((unsigned)std::max(nb, QG), (unsigned)(npairs + 1)), dim3(kNT), 0,
+                     S(stream), x, n, (int)rows, (int)nb, X, noise, decay, wet, klen, sr, force, (int)QG, Hs, snap);
+  int st = launch_status();
+  if (st || rows == 0) return st;
+  return upols_apply_spectra(X, rows, n, reinterpret_cast<const float*>(Hs), klen, false, y,
+                             X + (size_t)npairs * nb * kN, stream, false);
 }
 
 size_t upols_spectra_bytes(int64_t rows, int64_t n) {

@@ -5,7 +5,8 @@ synth modules.
 The control network before the path runs at inference on gfx950 kernels
 too: each MLP block is one matrix-core launch with its LayerNorm + LeakyReLU (core.mlp_block), the
 GRU recurrence is the step kernel (core.gru; its input projection a hipBLASLt GEMM), the two
-projections one hipBLASLt GEMM over their stacked weights, and the synthesis section of ``forward``
+projections one matrix-core launch over both layers' parameters (core.projections), and the synthesis
+section of ``forward``
 (decoder.py:106-125) one fused launch before the reverb.  Under autograd the MLPs and projections
 keep torch's modules; the GRU's BPTT runs on its backward step kernel.
 """
@@ -47,7 +48,7 @@ class GRUDecoder(nn.Module):
 def _gru(mod, hidden, h0):
     """mod.gru(hidden[, h0]) with the recurrence (and, under autograd, its BPTT) on the gfx950 step
     kernels; torch's GRU only for shapes outside the kernel's (hidden % 64 != 0)."""
-    if hidden.is_cuda and core.gru_supported(mod.gru):
+    if hidden.is_cuda and core.gru_supported(mod.gru) and _fp32_inference_ok(hidden, (mod.gru,)):
         return core.gru(hidden, mod.gru, h0)
     return mod.gru(hidden, h0) if h0 is not None else mod.gru(hidden)
 
@@ -61,6 +62,8 @@ def _mlp_fusable(seq, x):
     if _m._global_forward_hooks or _m._global_forward_pre_hooks or seq._forward_hooks or seq._forward_pre_hooks:
         return False
     if type(seq) is not nn.Sequential or type(seq).forward is not nn.Sequential.forward:
+        return False
+    if not _fp32_inference_ok(x, (seq,)):
         return False
     mods = list(seq)
     if len(mods) % 3:
@@ -156,53 +159,35 @@ def _synth_overridden(m, cls):
     return any(getattr(t, n, None) is not cls.__dict__[n] for n in ("forward", "get_controls"))
 
 
-def _shared_projection(self):
-    """(W, b): the two projections' weights and biases as ONE contiguous [H+1+NB, hidden] matrix and
-    [H+1+NB] vector whose row slices ARE harmonic_proj's and noise_proj's parameters (their ``.data``
-    point into it).  Every read is live — in-place updates through ``.data``, load_state_dict or an
-    optimizer step land in the shared storage — and the single GEMM needs no per-call concatenation.
-    The sharing is (re-)established whenever a parameter no longer views it (a fresh module, ``.to()``,
-    a replaced ``.data``): the current values are copied into a new shared buffer first."""
-    hp, npj = self.harmonic_proj, self.noise_proj
-    h1, n = hp.out_features, hp.out_features + npj.out_features
-    n_pad = -(-n // 64) * 64  # zero rows up to a multiple of 64: hipBLASLt runs 192 outputs in 28 us, 166 in 38.9
-    cached = self.__dict__.get("_proj_shared")
-    if cached is not None:
-        w, b = cached
-        if (w.device == hp.weight.device and w.dtype == hp.weight.dtype and
-                w.shape == (n_pad, hp.in_features) and hp.in_features == npj.in_features and
-                hp.weight.data_ptr() == w.data_ptr() and npj.weight.data_ptr() == w[h1:].data_ptr() and
-                hp.bias.data_ptr() == b.data_ptr() and npj.bias.data_ptr() == b[h1:].data_ptr() and
-                hp.weight.stride() == w.stride() and npj.weight.stride() == w.stride() and
-                hp.weight.shape == w[:h1].shape and npj.weight.shape == w[h1:n].shape):
-            return w, b
-    with torch.no_grad():
-        w = hp.weight.new_zeros(n_pad, hp.in_features)
-        b = hp.bias.new_zeros(n_pad)
-        w[:h1], w[h1:n] = hp.weight, npj.weight
-        b[:h1], b[h1:n] = hp.bias, npj.bias
-    hp.weight.data, npj.weight.data = w[:h1], w[h1:n]
-    hp.bias.data, npj.bias.data = b[:h1], b[h1:n]
-    self.__dict__["_proj_shared"] = (w, b)
-    return w, b
+def _fp32_inference_ok(x, mods):
+    """The fp32 network kernels apply: float32 input and parameters, and no autocast region (under
+    torch.autocast torch's modules run in the autocast dtype; these kernels compute in fp32 only)."""
+    if x.dtype != torch.float32 or any(p.dtype != torch.float32 for m in mods for p in m.parameters()):
+        return False
+    return not torch.is_autocast_enabled(x.device.type)
 
 
 def decoder_projections(self, hidden):
-    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden) — on the GPU as ONE GEMM over the
-    two projections' weights held in one shared buffer (``_shared_projection``; the two outputs are column
-    slices of it, which the fused synthesis kernel reads with their row stride).  Under autograd the
-    concatenation is differentiable, so the parameters receive their gradients as the reference's do."""
+    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden).  On the GPU at inference ONE
+    launch (core.projections: the fp32 matrix-core kernel reading both layers' own parameters — nothing
+    is copied, cached or rebound, so every write to a parameter, through ``.data`` included, is seen by
+    the next call); the two outputs are column slices of one buffer, which the fused synthesis kernel
+    reads with its row stride.  Under autograd the concatenated weights keep the call differentiable, so
+    the parameters receive their gradients as the reference's do."""
     hp, npj = self.harmonic_proj, self.noise_proj
     if not hidden.is_cuda or hp.bias is None or npj.bias is None or _hooked(hp) or _hooked(npj):
         return hp(hidden), npj(hidden)  # (module hooks see the calls the reference makes)
     ps = (hp.weight, hp.bias, npj.weight, npj.bias)
-    if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
-        w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
-    else:
-        w, b = _shared_projection(self)
-    out = torch.nn.functional.linear(hidden, w, b)  # hipBLASLt (a matrix-core kernel of this package's took 80 us)
     h1, n = hp.out_features, hp.out_features + npj.out_features
-    return out[..., :h1], out[..., h1:n]
+    if torch.is_grad_enabled() and (hidden.requires_grad or any(p.requires_grad for p in ps)):
+        w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
+        out = torch.nn.functional.linear(hidden, w, b)
+        return out[..., :h1], out[..., h1:n]
+    if _fp32_inference_ok(hidden, (hp, npj)):
+        r = core.projections(hidden, hp, npj)
+        if r is not None:
+            return r
+    return hp(hidden), npj(hidden)
 
 
 def decoder_synthesize(self, hidden, f0):

@@ -339,14 +339,16 @@ class ReverbApplyFn(_F):
 
 class ReverbFn(_F):
     """modules.py:21-35 Reverb.build_impulse + forward: gradients for the signal and for the
-    reverb's parameters (noise, decay, wet).  The forward's input spectra are kept for the
-    impulse gradient."""
+    reverb's parameters (noise, decay, wet).  The forward runs on the module's validated device IR
+    cache (modules.Reverb._forward_cached); its input spectra are kept for the impulse gradient."""
 
     @staticmethod
-    def forward(ctx, x, noise, decay, wet, spectrum, ir_length, sample_rate):
-        out, ws = core._reverb_apply_launch(x, spectrum, ir_length)
+    def forward(ctx, x, noise, decay, wet, run, ir_length, sample_rate):
+        out, ws, spectrum = run(x)  # modules.Reverb._forward_cached: (out, workspace, spectrum of the cache)
         ctx.save_for_backward(noise, decay, wet)
         ctx.ws = ws if any(ctx.needs_input_grad[1:4]) else None
+        # the cache's spectrum is rebuilt in place only when noise / decay / wet change, which autograd
+        # refuses between this forward and its backward (they are saved tensors)
         ctx.spectrum = spectrum
         ctx.T = x.shape[1]
         ctx.L, ctx.sr = int(ir_length), float(sample_rate)

@@ -16,7 +16,7 @@ LOSS_FUNCTIONS = ("multiscale_fft", "safe_log")
 METHODS = {
     "HarmonicSynth": ("get_controls", "forward"),
     "FilteredNoise": ("get_controls", "forward", "draw_noise"),
-    "Reverb": ("build_impulse", "forward", "_spectrum", "_spec_cache_key"),
+    "Reverb": ("build_impulse", "forward", "invalidate", "_spectrum", "_ir_cache", "_forward_cached"),
 }
 
 

@@ -32,44 +32,56 @@ class Reverb(nn.Module):
         self.wet = nn.Parameter(torch.tensor(float(initial_wet)))
         t = torch.arange(self.length) / self.sample_rate
         self.register_buffer("t", t.reshape(1, -1, 1))
-        self._spec_key = None
-        self._spec = None
-        # The IR spectrum is cached between forwards (the reference rebuilds it every call,
-        # modules.py:30-33).  The cache key holds the parameters' storage and autograd version
-        # counters: optimizer steps and in-place ops on the parameters invalidate it, writes through
-        # ``p.data`` (EMA copies, clamping via .data) do not — call invalidate() after those, or set
-        # cache_spectrum = False to rebuild on every forward as the reference does.
+        # The reference rebuilds the IR and its spectrum on every call (modules.py:30-33).  Here the
+        # spectrum lives in a device cache that the forward's first launch VALIDATES against the current
+        # parameters, bit for bit per IR window, rebuilding only the windows that changed
+        # (ddsp_hip_reverb_forward): every write to noise / decay / wet — optimizer steps, load_state_dict,
+        # writes through .data or other aliases — is seen by the next call, and unchanged parameters cost
+        # no rebuild.  cache_spectrum = False rebuilds every window on every call, as the reference does.
         self.cache_spectrum = True
 
     def invalidate(self):
-        """Drop the cached IR spectrum (rebuilt on the next forward)."""
-        self._spec_key = None
-        self._spec = None
+        """Drop the IR caches (not needed for correctness: every call validates its cache)."""
+        self.__dict__.pop("_ir_caches", None)
 
     def build_impulse(self):
         """modules.py:21-26 -> [1, length, 1]."""
         return core.reverb_build_impulse(self.noise, self.decay, self.wet, self.sample_rate)
 
-    def _spec_cache_key(self, n_samples):
-        return (n_samples, self.noise.device, self.noise.data_ptr(), self.noise._version,
-                self.decay._version, self.wet._version, self.decay.data_ptr(), self.wet.data_ptr())
+    def _ir_cache(self, n_samples):
+        """The device IR cache for inputs of n_samples (one per device and length: the crop/pad of
+        modules.py:31-33 depends on it), zero-filled when new."""
+        caches = self.__dict__.setdefault("_ir_caches", {})
+        key = (self.noise.device, int(n_samples), int(self.length))
+        c = caches.get(key)
+        if c is None:
+            c = torch.zeros(core.reverb_cache_bytes(n_samples, self.length), dtype=torch.uint8,
+                            device=self.noise.device)
+            caches[key] = c
+        return c
+
+    def _forward_cached(self, x):
+        """-> (out, workspace, spectrum): the reverb with the validated device cache (one launch group)."""
+        force = not getattr(self, "cache_spectrum", True)
+        return core.reverb_forward(x, self.noise, self.decay, self.wet, self.length, self.sample_rate,
+                                   Reverb._ir_cache(self, x.shape[1]), force)
 
     def _spectrum(self, n_samples):
-        key = Reverb._spec_cache_key(self, n_samples)
-        if key != getattr(self, "_spec_key", None) or not getattr(self, "cache_spectrum", True):
-            with torch.no_grad():  # build_impulse (modules.py:21-26) and its spectra: one launch
-                self._spec = core.reverb_impulse_spectrum(self.noise, self.decay, self.wet, self.sample_rate,
-                                                          n_samples)
-            self._spec_key = key
-        return self._spec
+        """The current IR spectrum for inputs of n_samples (validated / rebuilt on the device first); a view
+        of the cache, which later calls update in place when the parameters change."""
+        with torch.no_grad():
+            return core.reverb_forward(None, self.noise, self.decay, self.wet, self.length, self.sample_rate,
+                                       Reverb._ir_cache(self, n_samples), not getattr(self, "cache_spectrum", True),
+                                       n_samples=n_samples)[2]
 
     def forward(self, x):
         """modules.py:28-35: IR padded/cropped to len(x), causal convolution truncated to len(x).
         Under autograd the signal and the reverb parameters (noise, decay, wet) get gradients."""
-        spec = Reverb._spectrum(self, x.shape[1])
         if core._wants_grad(x, self.noise, self.decay, self.wet):
-            return grad.ReverbFn.apply(x, self.noise, self.decay, self.wet, spec, self.length, self.sample_rate)
-        return core.reverb_apply(x, spec, self.length)
+            return grad.ReverbFn.apply(x, self.noise, self.decay, self.wet, lambda v: Reverb._forward_cached(self, v),
+                                       self.length, self.sample_rate)
+        with torch.no_grad():
+            return Reverb._forward_cached(self, x)[0]
 
 
 class HarmonicSynth(nn.Module):

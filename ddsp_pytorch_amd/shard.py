@@ -69,8 +69,8 @@ def synthesize_sharded(synth, inputs, rank, world, gather=False, dst=0):
 def broadcast_module(module, src=0, group=None):
     """Broadcast a module's parameters and buffers (the reverb IR parameters) from ``src``.
 
-    Each tensor is received into a copy and written back with copy_ so its version counter
-    moves and caches keyed on it (Reverb's IR spectrum) are invalidated."""
+    Each tensor is received into a copy and written back with copy_ (the Reverb's device IR cache
+    validates itself against the parameters on its next call)."""
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             tmp = t.detach().clone()

@@ -188,6 +188,22 @@ int ddsp_hip_reverb_spectrum(const float* impulse, int64_t ir_length, int64_t n_
 int ddsp_hip_reverb_apply(const float* x, const float* spectrum, float* out, int64_t batch,
                           int64_t n_samples, int64_t ir_length, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* modules.py:21-35 Reverb.forward (build_impulse, crop/pad to n_samples, fft_convolve) with the IR's partition
+ * spectra cached on the device and VALIDATED there on every call: `cache` (caller-owned device memory of
+ * ddsp_hip_reverb_cache_bytes bytes, zero-filled once: a zeroed cache holds nothing) keeps, per IR window,
+ * the spectrum and a bit-exact copy of the inputs it was built from (the window's noise taps, decay, wet,
+ * sample_rate).  The input transform's launch compares them with the current parameters and rebuilds the
+ * windows that differ, so any write to the parameters (optimizer steps, writes through aliases such as
+ * `.data`) is seen by the next call, and unchanged parameters cost no rebuild.  force != 0 rebuilds every
+ * window (the reference's every-call rebuild).  batch == 0 validates the cache only.  The cache's first
+ * ddsp_hip_reverb_spectrum_floats(n_samples, ir_length) floats are then the current spectrum (as
+ * ddsp_hip_reverb_impulse_spectrum writes it, bit for bit; used by ddsp_hip_reverb_backward).  Workspace:
+ * ddsp_hip_reverb_workspace_size; it then holds x's input spectra as after ddsp_hip_reverb_apply. */
+size_t ddsp_hip_reverb_cache_bytes(int64_t n_samples, int64_t ir_length);
+int ddsp_hip_reverb_forward(const float* x, const float* noise, const float* decay, const float* wet,
+                            int64_t ir_length, float sample_rate, int force, void* cache, size_t cache_bytes,
+                            float* out, int64_t batch, int64_t n_samples, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* ---------------- the decoder network for a few frames: core.py:122-129, decoder.py:43-68 ----------------
  * One Linear for rows <= 8 frames (the realtime stream's 1024-sample calls, ddsp_model.cpp:32-52)
@@ -224,11 +240,6 @@ typedef struct ddsp_hip_dense_problem {
 } ddsp_hip_dense_problem;
 int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream);
 
-/* ddsp/core.py:122-129 (one MLP block after its Linear, decoder.py:25-42): y = LeakyReLU(LayerNorm(h))
- * per row of cols features, h = x [rows, x_ld] or, with w1/b1 (a Linear with ONE input feature),
- * h = x[r] * w1 + b1 formed on the fly.  gamma/beta: the LayerNorm's affine; eps and the negative
- * slope as in torch (1e-5, 0.01).  y [rows, y_ld] may be a column slice of a wider buffer.  One pass
- * instead of torch's two; cols 512 or 1024 with 16-byte aligned rows, else DDSP_HIP_ERANGE. */
 /* ddsp/core.py:122-129: one whole MLP block, y = LeakyReLU(LayerNorm(x W^T + b)), W [out, w_ld] the
  * nn.Linear weight, for out_features = 512 (else DDSP_HIP_ERANGE): the Linear on the fp32 matrix cores,
  * LayerNorm + LeakyReLU in its epilogue.  e0/e1 (nullable, per-row scalars at stride e_ld) add
@@ -238,9 +249,25 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
                        const float* bias, const float* e0, const float* e1, int64_t e_ld, const float* gamma,
                        const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                        int64_t out_features, void* stream);
+/* ddsp/core.py:122-129 (one MLP block after its Linear, decoder.py:25-42): y = LeakyReLU(LayerNorm(h))
+ * per row of cols features, h = x [rows, x_ld] or, with w1/b1 (a Linear with ONE input feature),
+ * h = x[r] * w1 + b1 formed on the fly.  gamma/beta: the LayerNorm's affine; eps and the negative
+ * slope as in torch (1e-5, 0.01).  y [rows, y_ld] may be a column slice of a wider buffer.  One pass
+ * instead of torch's two; cols 512 or 1024 with 16-byte aligned rows, else DDSP_HIP_ERANGE. */
 int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1, const float* b1, const float* gamma,
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);
+
+/* decoder.py:106-117: param = harmonic_proj(hidden), magnitudes = noise_proj(hidden) as ONE launch over
+ * the two nn.Linear layers' own parameters (no concatenated weight copy is kept or rebuilt):
+ * y[r][c] = b1[c] + sum_k x[r][k] w1[c][k] for c < n1, b2[c-n1] + sum_k x[r][k] w2[c-n1][k] for
+ * n1 <= c < n1 + n2; x [rows, x_ld], w1 [n1, w1_ld], w2 [n2, w2_ld], y [rows, y_ld] (y_ld >= n1 + n2:
+ * param and magnitudes are its column slices, read by ddsp_hip_synth_frames_controls with that row
+ * stride).  fp32 matrix cores (exact fp32 products and sums); n1 + n2 <= 224, K % 4 == 0 and 16-byte
+ * aligned x / w rows, else DDSP_HIP_ERANGE (callers keep torch's Linear). */
+int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, const float* w1, int64_t w1_ld,
+                         const float* b1, int64_t n1, const float* w2, int64_t w2_ld, const float* b2, int64_t n2,
+                         float* y, int64_t y_ld, int64_t rows, void* stream);
 
 /* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
  * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,

@@ -195,6 +195,9 @@ def main():
     grad_goldens(ddsp, decoder, modules, sr)
     realtime_goldens(decoder, sr)
     autoencoder_golden(sr)
+    decoder512_golden(sr)
+    autoencoder512_golden(sr)
+    grad512_golden(sr)
 
 
 @torch.no_grad()
@@ -315,6 +318,103 @@ def autoencoder_golden(sr):
          magnitudes=o["noise_ctrls"]["magnitudes"], **sd)
 
 
+def state_dict_crcs(model):
+    """Per-tensor CRC32 of the state_dict's raw bytes (and shape): the fixture pins the parameters a
+    seeded constructor draws without storing them (4.3 M floats at the shipped hidden size)."""
+    import zlib
+    out = {}
+    for k, v in model.state_dict().items():
+        a = np.ascontiguousarray(v.detach().cpu().numpy())
+        out["crc." + k] = np.uint32(zlib.crc32(a.tobytes()))
+        out["shape." + k] = np.asarray(a.shape, dtype=np.int64)
+    return out
+
+
+@torch.no_grad()
+def decoder512_golden(sr):
+    """g10: DDSPDecoder at the reference's shipped network size (config.yaml:16-21: hidden 512,
+    n_harmonic 64, n_bands 65, block 512, reverb on), built after torch.manual_seed(0), forward on
+    B=2, F=24 with the noise drawn after manual_seed(123).  The state_dict is stored as per-tensor
+    CRC32s only: the test rebuilds the module under the same seed and checks them.  At this size the
+    GPU route runs the H=512 GRU step kernel, the 512-wide MLP blocks and the projection kernel."""
+    from ddsp.models import decoder
+    torch.manual_seed(0)
+    model = decoder.DDSPDecoder(512, 64, 65, sr, 512, True).eval()
+    f0, loudness, _, _ = synth_inputs(20, 2, 24, 64, 65)
+    torch.manual_seed(123)
+    noise_in = torch.rand(2, 24, 512) * 2 - 1  # the draw FilteredNoise.forward makes next
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness})
+    save("g10_decoder512", hidden_size=512, n_harmonic=64, n_bands=65, sample_rate=sr, block_size=512,
+         model_seed=0, noise_seed=123, pitch=f0, loudness=loudness, noise_in=noise_in,
+         signal=o["signal"], noise=o["noise"], harmonic_audio=o["harmonic_audio"],
+         amplitudes=o["harmonic_ctrls"]["amplitudes"],
+         distribution=o["harmonic_ctrls"]["harmonic_distribution"],
+         magnitudes=o["noise_ctrls"]["magnitudes"], **state_dict_crcs(model))
+
+
+@torch.no_grad()
+def autoencoder512_golden(sr):
+    """g9b: DDSPAutoencoder (encoder.py:29-103) at hidden 512, seeded like g10, B=2, F=16; the
+    state_dict as CRC32s.  Reaches the 30-input encoder GRU and the z-conditioned decoder GRU
+    (input 3H) on the step kernels, z_mlp's K=16 block and out_mlp's extras path."""
+    from ddsp.models import encoder
+    torch.manual_seed(0)
+    model = encoder.DDSPAutoencoder(512, 100, 65, sr, 512, True).eval()
+    f0, loudness, _, _ = synth_inputs(21, 2, 16, 100, 65)
+    mfcc = torch.randn(2, 16, 30, generator=torch.Generator().manual_seed(22)) * 10.0
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness, "mfcc": mfcc})
+    save("g9b_autoencoder512", hidden_size=512, n_harmonic=100, n_bands=65, sample_rate=sr, block_size=512,
+         model_seed=0, noise_seed=123, pitch=f0, loudness=loudness, mfcc=mfcc, signal=o["signal"],
+         noise=o["noise"], harmonic_audio=o["harmonic_audio"], z=o["z"],
+         amplitudes=o["harmonic_ctrls"]["amplitudes"],
+         distribution=o["harmonic_ctrls"]["harmonic_distribution"],
+         magnitudes=o["noise_ctrls"]["magnitudes"], **state_dict_crcs(model))
+
+
+@torch.enable_grad()
+def grad512_golden(sr):
+    """g6b: the reference's autograd through DDSPDecoder at the shipped size (hidden 512, 64 harmonics),
+    B=2, F=8, loss = sum(signal * w).  Stored: the gradients at the two projections' outputs in full, and
+    per parameter the gradient's L2 norm plus 2048 entries at seeded indices (every entry for tensors of
+    at most 2048 elements) — enough to pin each gradient without storing 4.3 M floats."""
+    from ddsp.models import decoder
+    torch.manual_seed(0)
+    model = decoder.DDSPDecoder(512, 64, 65, sr, 512, True)
+    acts = {}
+
+    def keep(name):
+        def hook(mod, inp, out):
+            out.retain_grad()
+            acts[name] = out
+        return hook
+
+    model.harmonic_proj.register_forward_hook(keep("param"))
+    model.noise_proj.register_forward_hook(keep("mags"))
+    f0, loudness, _, _ = synth_inputs(23, 2, 8, 64, 65)
+    torch.manual_seed(123)
+    o = model({"pitch": f0, "loudness": loudness})
+    w = torch.randn(o["signal"].shape, generator=torch.Generator().manual_seed(24))
+    (o["signal"] * w).sum().backward()
+    arrays = {}
+    gi = torch.Generator().manual_seed(25)
+    for k, v in model.named_parameters():
+        if v.grad is None:
+            continue
+        flat = v.grad.reshape(-1)
+        if flat.numel() <= 2048:
+            idx = torch.arange(flat.numel())
+        else:
+            idx = torch.randperm(flat.numel(), generator=gi)[:2048].sort().values
+        arrays["gidx." + k] = idx.to(torch.int32)
+        arrays["gval." + k] = flat[idx]
+        arrays["gnorm." + k] = flat.double().norm()
+    save("g6b_grad_decoder512", hidden_size=512, n_harmonic=64, n_bands=65, sample_rate=sr, block_size=512,
+         model_seed=0, noise_seed=123, pitch=f0, loudness=loudness, weight=w, signal=o["signal"].detach(),
+         grad_param=acts["param"].grad, grad_mags=acts["mags"].grad, **arrays, **state_dict_crcs(model))
+
+
 def masked_loss_golden(ddsp):
     """g7b: train.py:70-76's loss restricted to the well-conditioned bins, on g7's signals, computed by
     the reference's multiscale_fft / safe_log (core.py:10-41) in fp32 with autograd.  The bins with
@@ -353,5 +453,11 @@ if __name__ == "__main__":
     elif sys.argv[1:] == ["g7b"]:  # only the masked-loss fixture (reads g7)
         torch.set_num_threads(8)
         masked_loss_golden(import_reference()[0])
+    elif sys.argv[1:] == ["g10"]:  # only the shipped-size fixtures (g10, g9b, g6b)
+        torch.set_num_threads(8)
+        import_reference()
+        decoder512_golden(48000)
+        autoencoder512_golden(48000)
+        grad512_golden(48000)
     else:
         main()

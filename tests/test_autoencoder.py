@@ -4,9 +4,12 @@ size 32, seeded, with its state_dict and an MFCC input tensor).
 
 CPU: the state_dict layout is the reference's (every g9 key loads, nothing extra) and the encoder and
 z-conditioned decoder network reproduce the reference's z and hidden state on the host (plain torch:
-LayerNorm / GRU / Linear are not on the accelerated path).  GPU: the whole forward — the encoder and
-decoder GRUs on the step kernels, the projections as one GEMM, the synthesis section as the fused
-launch — matches signal, harmonic, noise, z and the control dicts (north_star: 1e-5 RMS)."""
+LayerNorm / GRU / Linear are not on the accelerated path).  GPU: the whole forward — the projections as one
+GEMM, the synthesis section as the fused launch — matches signal, harmonic, noise, z and the control dicts
+(north_star: 1e-5 RMS).  At g9's hidden size 32 the network itself stays on torch's modules (the GRU step
+kernels need hidden % 64 == 0, the MLP block kernel 512 outputs); the shipped size (hidden 512), where the
+encoder and decoder GRUs run the step kernels and the MLPs the block kernel, is pinned by g9b in
+tests/test_decoder512.py."""
 import numpy as np
 import pytest
 import torch

@@ -1,53 +1,47 @@
-"""Host logic of the decoder's fused route (no GPU needed): the shared projection buffer stays live
-under every way a parameter can change, and hooked / overridden synth modules keep their module calls
-(ADVICE r03)."""
+"""Host logic of the decoder's fused route (no GPU needed): the projections are never rebound, copied or
+cached by the module (the round-4 shared padded buffer re-pointed the parameters' storage), the
+fp32-only network kernels step aside for other dtypes and autocast, and hooked / overridden synth modules
+keep their module calls."""
+import copy
+import io
+
 import torch
 
 import ddsp_pytorch_amd as dd
-from ddsp_pytorch_amd.decoder import _shared_projection, _synth_overridden
+from ddsp_pytorch_amd.decoder import _fp32_inference_ok, _synth_overridden
 
 
-def _cat(m):
-    return (torch.cat([m.harmonic_proj.weight, m.noise_proj.weight]).detach(),
-            torch.cat([m.harmonic_proj.bias, m.noise_proj.bias]).detach())
-
-
-def _sp(m):
-    """The shared buffer's live rows (it is zero-padded to a multiple of 64 outputs for the GEMM)."""
-    w, b = _shared_projection(m)
-    n = m.harmonic_proj.out_features + m.noise_proj.out_features
-    assert w.shape[0] % 64 == 0 and not w[n:].any() and not b[n:].any()
-    return w[:n], b[:n]
-
-
-def test_shared_projection_is_live():
+def test_projections_leave_parameters_alone():
+    """decoder_projections keeps no state on the module: parameters keep their own storage, the module's
+    __dict__ gains nothing, deepcopy / state_dict / torch.save see exactly the reference's tensors."""
     torch.manual_seed(0)
     m = dd.DDSPDecoder(32, 10, 9, 48000, 64, False)
-    w, b = _sp(m)
-    assert torch.equal(w, _cat(m)[0]) and torch.equal(b, _cat(m)[1])
-    # the parameters are views of the shared buffer: in-place writes through .data are seen
-    m.harmonic_proj.weight.data.mul_(2.0)
-    w2, b2 = _sp(m)
-    assert w2.data_ptr() == w.data_ptr() and torch.equal(w2, _cat(m)[0])
-    m.noise_proj.bias.data.copy_(torch.arange(9.0))
-    assert torch.equal(_sp(m)[1], _cat(m)[1])
-    # load_state_dict copies into the parameters in place
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
-    sd["harmonic_proj.weight"].fill_(0.5)
-    m.load_state_dict(sd)
-    assert torch.equal(_sp(m)[0], _cat(m)[0])
-    # a replaced .data (or a fresh module) is re-shared with its current values
-    m.noise_proj.weight.data = torch.randn(9, 32)
-    w3, _ = _sp(m)
-    assert w3.data_ptr() != w.data_ptr() and torch.equal(w3, _cat(m)[0])
-    m.harmonic_proj = torch.nn.Linear(32, 11)
-    assert torch.equal(_sp(m)[0], _cat(m)[0])
-    # an optimizer step updates the shared storage too
-    opt = torch.optim.SGD(m.parameters(), lr=0.1)
-    for p in m.parameters():
-        p.grad = torch.ones_like(p)
-    opt.step()
-    assert torch.equal(_sp(m)[0], _cat(m)[0])
+    ptrs = {k: p.data_ptr() for k, p in m.named_parameters()}
+    keys = set(m.__dict__)
+    with torch.no_grad():
+        hp, npj = dd.decoder.decoder_projections(m, torch.randn(2, 3, 32))
+    assert hp.shape == (2, 3, 11) and npj.shape == (2, 3, 9)
+    assert {k: p.data_ptr() for k, p in m.named_parameters()} == ptrs and set(m.__dict__) == keys
+    sd = m.state_dict()
+    assert sd["harmonic_proj.weight"].shape == (11, 32) and sd["noise_proj.bias"].shape == (9,)
+    assert sd["harmonic_proj.weight"].untyped_storage().data_ptr() != sd["noise_proj.weight"].untyped_storage().data_ptr()
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    n_floats = sum(v.numel() for v in sd.values())
+    assert len(buf.getvalue()) < 4 * n_floats + 64 * 1024  # no padded shared buffer serialised
+    c = copy.deepcopy(m)
+    for (k, a), b in zip(m.state_dict().items(), c.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+def test_fp32_inference_guard():
+    lin = torch.nn.Linear(4, 3)
+    x = torch.randn(2, 4)
+    assert _fp32_inference_ok(x, (lin,))
+    assert not _fp32_inference_ok(x.double(), (lin,))
+    assert not _fp32_inference_ok(x, (torch.nn.Linear(4, 3).half(),))
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        assert not _fp32_inference_ok(x, (lin,))
 
 
 def test_synth_overridden():

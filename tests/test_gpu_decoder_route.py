@@ -54,3 +54,24 @@ def test_hooked_synth_module_keeps_module_calls(dd):
         h.remove()
     assert seen, "the hook did not fire: the fused route skipped the module call"
     torch.testing.assert_close(hooked, plain, rtol=1e-5, atol=2e-6)
+
+
+def test_forward_leaves_parameter_storage_alone(dd, tmp_path):
+    """A no-grad GPU forward (the projection kernel reads harmonic_proj / noise_proj in place) changes
+    nothing on the module: same storages, safetensors can save the state_dict (tensors that shared one
+    buffer would be refused), torch.save holds only the reference's tensors, deepcopy is independent."""
+    import copy
+    safetensors = pytest.importorskip("safetensors.torch")
+    torch.manual_seed(0)
+    m = dd.DDSPDecoder(64, 20, 17, 48000, 256, True).cuda().eval()
+    ptrs = {k: p.data_ptr() for k, p in m.named_parameters()}
+    a = _run(m, _batch())
+    assert {k: p.data_ptr() for k, p in m.named_parameters()} == ptrs
+    safetensors.save_file({k: v.contiguous() for k, v in m.state_dict().items()}, str(tmp_path / "m.safetensors"))
+    torch.save(m.state_dict(), tmp_path / "m.pt")
+    n_bytes = sum(4 * v.numel() for v in m.state_dict().values())
+    assert (tmp_path / "m.pt").stat().st_size < n_bytes + 64 * 1024
+    c = copy.deepcopy(m)
+    c.harmonic_proj.weight.data.mul_(3.0)
+    b = _run(m, _batch())
+    torch.testing.assert_close(a, b, rtol=0, atol=0)

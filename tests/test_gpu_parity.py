@@ -283,7 +283,7 @@ def test_decoder_outside_fused_envelope(dd):
 def _reference_shaped_modules():
     """Classes carrying exactly the reference's instance attributes (modules.py:7-128: the
     constructors' fields, parameters and buffers) and none of this package's extras
-    (noise_mode, _spec_key, _spec, cache_spectrum) - what install() finds on real reference
+    (noise_mode, _ir_caches, cache_spectrum) - what install() finds on real reference
     instances.  Their methods are placeholders that install() replaces."""
     import types
     import torch.nn as nn

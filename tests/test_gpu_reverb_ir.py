@@ -70,3 +70,66 @@ def test_ir_rebuild_every_call_and_after_updates(dd):
             syn.reverb.wet.sub_(0.1)
         out = syn(*args)
         assert torch.equal(out, inline())
+
+
+@pytest.mark.parametrize("L,T", [(48000, 102400), (48000, 24000), (4800, 9600)])
+def test_device_cache_is_the_impulse_spectrum(dd, L, T):
+    """The module's device cache (ddsp_hip_reverb_forward) holds ddsp_hip_reverb_impulse_spectrum's
+    spectrum bit for bit, after the first call, after a rebuild, and in the every-call (force) mode."""
+    torch.manual_seed(1)
+    rv = dd.Reverb(L, 48000, initial_wet=0.3, initial_decay=3.0).cuda()
+    x = torch.randn(3, T, 1, device="cuda")
+    with torch.no_grad():
+        a = rv(x)
+        ref = dd.core.reverb_impulse_spectrum(rv.noise, rv.decay, rv.wet, 48000, T)
+        assert torch.equal(rv._spectrum(T), ref)
+        rv.cache_spectrum = False
+        b = rv(x)
+        assert torch.equal(a, b) and torch.equal(rv._spectrum(T), ref)
+        assert torch.equal(a, dd.core.reverb_apply(x, ref, L))
+
+
+def test_device_cache_sees_writes_through_data(dd):
+    """an EMA-style update through ``p.data`` (no autograd version bump) between two
+    forwards is seen by the second — the launch compares the parameters with the cached spectrum's inputs
+    bit for bit — and one changed tap rebuilds only what it touches yet equals a fresh module."""
+    torch.manual_seed(1)
+    rv = dd.Reverb(48000, 48000).cuda()
+    x = torch.randn(4, 102400, 1, device="cuda")
+    with torch.no_grad():
+        a = rv(x)
+        for p in (rv.noise, rv.decay, rv.wet):  # EMA toward a shadow copy, through .data
+            p.data.mul_(0.999).add_(0.001 * torch.randn_like(p))
+        b = rv(x)
+        rv.noise.data[30000, 0] += 0.25  # one tap, in one window pair
+        c = rv(x)
+    assert not torch.equal(a, b) and not torch.equal(b, c)
+    for out in (c,):
+        fresh = dd.Reverb(48000, 48000).cuda()
+        fresh.load_state_dict(rv.state_dict())
+        with torch.no_grad():
+            ref = fresh(x)
+        assert torch.equal(out, ref)
+    with torch.no_grad():  # the cached spectrum is rebuilt bit-identically to the one-launch rebuild
+        assert torch.equal(rv._spectrum(102400), dd.core.reverb_impulse_spectrum(rv.noise, rv.decay, rv.wet, 48000,
+                                                                                  102400))
+
+
+def test_device_cache_training_step(dd):
+    """Under autograd (ReverbFn) with an optimizer step between forwards, the cache follows the updated
+    parameters, and the gradients equal those of a module rebuilding every call."""
+    torch.manual_seed(1)
+    a = dd.Reverb(4800, 48000, initial_wet=0.5, initial_decay=3.0).cuda()
+    b = dd.Reverb(4800, 48000, initial_wet=0.5, initial_decay=3.0).cuda()
+    b.load_state_dict(a.state_dict())
+    b.cache_spectrum = False
+    oa, ob = torch.optim.SGD(a.parameters(), lr=0.05), torch.optim.SGD(b.parameters(), lr=0.05)
+    x = torch.randn(3, 9600, 1, device="cuda")
+    w = torch.randn(3, 9600, 1, device="cuda")
+    for _ in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            (m(x) * w).sum().backward()
+            o.step()
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            assert torch.equal(pa, pb)

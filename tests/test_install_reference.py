@@ -5,7 +5,7 @@ The reference is imported with SURVEY.md §8(c)'s placeholder modules for libros
 pytorch_lightning (imported by ddsp/core.py:5-6 and ddsp/data.py:5, unused by the synthesis
 path).  After install(ddsp), every method swapped onto the reference's classes must resolve on
 real reference instances: each `self.<attr>` the swapped method reads must exist on the
-instance (the reference's __init__ never sets noise_mode, _spec_key, _spec or cache_spectrum, so
+instance (the reference's __init__ never sets noise_mode, _ir_caches or cache_spectrum, so
 those may only be read through getattr with a default).  The functions must refuse CPU tensors
 loudly (no CPU fallback).  uninstall() restores the reference exactly.
 """

@@ -24,14 +24,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # their own access pattern (MI355X_MICROARCH.md: other widths "uncalibrated: calibrate"): the
 # inverse reads the Y spectra exactly once (51.2 MB at config 2) and reports 25.7 MB; the forward
 # reads the signal exactly once (26.2 MB) and reports 12.9 MB
-WIDE_READS = ("harmonic_samples_tiled_kernel", "upols_forward_kernel", "upols_inverse_kernel",
+WIDE_READS = ("harmonic_samples_tiled_kernel", "upols_forward_kernel", "upols_forward_ir_kernel", "upols_inverse_kernel",
               "upols_mac_kernel", "upols_mac_ring_kernel")
 REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch of it
     "synth_frame_kernel": ("synth_frame_kernel",),
     "harmonic_frames_kernel": ("harmonic_frames_kernel",),
     "harmonic_samples_kernel": ("phase_chunk_sums_kernel", "harmonic_samples_tiled_kernel"),
     "filtered_noise_kernel": ("filtered_noise_kernel",),
-    "reverb": ("upols_forward_kernel", "upols_mac_kernel", "upols_mac_ring_kernel", "upols_inverse_kernel"),
+    "reverb": ("upols_forward_kernel", "upols_forward_ir_kernel", "upols_mac_kernel", "upols_mac_ring_kernel", "upols_inverse_kernel"),
 }
 
 
