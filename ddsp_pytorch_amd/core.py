@@ -569,13 +569,20 @@ def gru(x, gru_module, h0=None):
 
 def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates):
     """The layer's forward on the device: the input projection for every step as one GEMM, then the
-    recurrence on ddsp_hip_gru_forward's step kernels (a form with each step's projection inside the
-    step launch measured slower: 13.3 vs 7.4-7.8 us per step)."""
+    recurrence as one persistent launch (ddsp_hip_gru_forward_persistent, hidden 512 and batch <= 64) or
+    on ddsp_hip_gru_forward's step kernels (a form with each step's projection inside the step launch
+    measured slower: 13.3 vs 7.4-7.8 us per step)."""
     B, T, I = x.shape
     H = w_hh.shape[1]
     xp = torch.addmm(b_ih, _c(x).reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
-    _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out),
-              _lib.ptr(h_last), _lib.ptr(gates), B, T, H, _lib.stream_of(out))
+    args = (_lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out), _lib.ptr(h_last),
+            _lib.ptr(gates), B, T, H)
+    # hidden 512, batch <= 64: the whole recurrence as one persistent launch (W_hh resident in LDS, h handed
+    # between the workgroups of a group); otherwise (ERANGE) one launch per step
+    ws = _workspace(_lib.query("gru_persistent_workspace_size"), out.device)
+    st = _lib.call("gru_forward_persistent", *args, _lib.ptr(ws), ws.numel(), _lib.stream_of(out), allow=(ERANGE,))
+    if st == ERANGE:
+        _lib.call("gru_forward", *args, _lib.stream_of(out))
 
 
 def mlp_block(x, linear, norm, act, out=None, extras=()):

@@ -423,7 +423,7 @@ __global__ void __launch_bounds__(512) mlp_block_kernel(
 // wave w computes row tile w & 3 against half w >> 2 of the column tiles (one A fragment shared by up
 // to 8 B tiles per LDS read).  Columns past n1 + n2 are zero weights, never stored.
 constexpr int kProjRows = 64;
-constexpr int kProjKC = 32;
+constexpr int kProjKC = 32;  // K per LDS stage (two stages in LDS: one barrier per stage)
 constexpr int kProjLd = kProjKC + 4;
 constexpr int kProjMaxTiles = 14;  // 224 columns (15 and 16 tiles spilled)
 
@@ -434,9 +434,11 @@ __global__ void __launch_bounds__(512) projections_kernel(
     const float* __restrict__ b2, int n2, float* __restrict__ y, int64_t y_ld, int64_t R) {
   constexpr int NA = (NT + 1) / 2;               // column tiles per wave (an odd NT pads one zero tile)
   constexpr int NC = 2 * NA * 16;                // columns staged
-  constexpr int NBL = (NC * 8 + 511) / 512;      // W float4 loads per thread per stage
-  __shared__ __attribute__((aligned(16))) float As[kProjRows * kProjLd];
-  __shared__ __attribute__((aligned(16))) float Bs[NC * kProjLd];
+  constexpr int KV = kProjKC / 4;                 // float4s per row per stage
+  constexpr int NBL = (NC * KV + 511) / 512;     // W float4 loads per thread per stage
+  constexpr int NAL = kProjRows * KV / 512;      // x float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) float As[2][kProjRows * kProjLd];
+  __shared__ __attribute__((aligned(16))) float Bs[2][NC * kProjLd];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int q = lane >> 4, l16 = lane & 15;
   const int rt = wv & 3, tile0 = (wv >> 2) * NA;
@@ -444,54 +446,69 @@ __global__ void __launch_bounds__(512) projections_kernel(
   const int nc = (K + kProjKC - 1) / kProjKC, ncol = n1 + n2;
   // every load is unconditional from a valid address (clamped row / column / k) and zeroed by a
   // select past the matrix: no divergent branches around the loads
-  const int arow = t >> 3;
-  const float* xrow = x + (r0 + arow < R ? r0 + arow : R - 1) * x_ld;
+  const float* xr[NAL];
+#pragma unroll
+  for (int i = 0; i < NAL; ++i) {
+    const int arow = (t + 512 * i) / KV;
+    xr[i] = x + (r0 + arow < R ? r0 + arow : R - 1) * x_ld;
+  }
   const float* wr[NBL];
   bool wok[NBL];
 #pragma unroll
   for (int i = 0; i < NBL; ++i) {
-    const int col = (t + 512 * i) >> 3;
+    const int col = (t + 512 * i) / KV;
     const int cc = col < ncol ? col : ncol - 1;
     wr[i] = cc < n1 ? w1 + (int64_t)cc * w1_ld : w2 + (int64_t)(cc - n1) * w2_ld;
     wok[i] = col < ncol;
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 sa, sb[NBL];
+  float4 sa[NAL], sb[NBL];
   auto load = [&](int c) {
-    const int k = c * kProjKC + 4 * (t & 7);
+    const int k = c * kProjKC + 4 * (t % KV);  // (512 * i) % KV == 0: the same k for every i
     const int kk = k < K ? k : K - 4;
-    sa = *reinterpret_cast<const float4*>(xrow + kk);
-    if (k >= K) sa = z4;
+#pragma unroll
+    for (int i = 0; i < NAL; ++i) {
+      sa[i] = *reinterpret_cast<const float4*>(xr[i] + kk);
+      if (k >= K) sa[i] = z4;
+    }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
       sb[i] = *reinterpret_cast<const float4*>(wr[i] + kk);
       if (!wok[i] || k >= K) sb[i] = z4;
     }
   };
-  auto store = [&]() {
-    *reinterpret_cast<float4*>(&As[arow * kProjLd + 4 * (t & 7)]) = sa;
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NAL; ++i) {
+      const int f = t + 512 * i;
+      *reinterpret_cast<float4*>(&As[buf][(f / KV) * kProjLd + 4 * (f % KV)]) = sa[i];
+    }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
       const int f = t + 512 * i;
-      if (NBL * 512 == NC * 8 || f < NC * 8) *reinterpret_cast<float4*>(&Bs[(f >> 3) * kProjLd + 4 * (f & 7)]) = sb[i];
+      if (NBL * 512 == NC * KV || f < NC * KV)
+        *reinterpret_cast<float4*>(&Bs[buf][(f / KV) * kProjLd + 4 * (f % KV)]) = sb[i];
     }
   };
   f32x4_t acc[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // two LDS stages: stage c is read from buffer c & 1 while stage c + 1 is stored into the other one;
+  // the one barrier per stage (after that store) also ends every wave's reads of stage c - 1's buffer
   load(0);
+  store(0);
+  __syncthreads();
+  if (nc > 1) load(1);
   for (int c = 0; c < nc; ++c) {
-    __syncthreads();  // every wave is done reading the previous stage
-    store();
-    __syncthreads();
-    if (c + 1 < nc) load(c + 1);  // in flight under this stage's MFMAs
+    const float* Ab = As[c & 1];
+    const float* Bb = Bs[c & 1];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float4 af = *reinterpret_cast<const float4*>(&As[(16 * rt + l16) * kProjLd + 16 * h + 4 * q]);
+    for (int h = 0; h < kProjKC / 16; ++h) {
+      const float4 af = *reinterpret_cast<const float4*>(&Ab[(16 * rt + l16) * kProjLd + 16 * h + 4 * q]);
       float4 bf[NA];
 #pragma unroll
       for (int j = 0; j < NA; ++j)
-        bf[j] = *reinterpret_cast<const float4*>(&Bs[(16 * (tile0 + j) + l16) * kProjLd + 16 * h + 4 * q]);
+        bf[j] = *reinterpret_cast<const float4*>(&Bb[(16 * (tile0 + j) + l16) * kProjLd + 16 * h + 4 * q]);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const float a = s == 0 ? af.x : s == 1 ? af.y : s == 2 ? af.z : af.w;
@@ -501,6 +518,11 @@ __global__ void __launch_bounds__(512) projections_kernel(
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
         }
       }
+    }
+    if (c + 1 < nc) {
+      store((c + 1) & 1);
+      __syncthreads();
+      if (c + 2 < nc) load(c + 2);  // lands under stage c + 1's MFMAs
     }
   }
   // acc[j][e] is row 16 rt + 4 q + e, column 16 (tile0 + j) + l16
@@ -521,7 +543,11 @@ template <int NT>
 void launch_projections(dim3 grid, hipStream_t st, const float* x, int64_t x_ld, int K, const float* w1,
                         int64_t w1_ld, const float* b1, int n1, const float* w2, int64_t w2_ld, const float* b2,
                         int n2, float* y, int64_t y_ld, int64_t R) {
-  hipLaunchKernelGGL(projections_kernel<NT>, grid, dim3(512), 0, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2,
+  // one workgroup per CU: with 200 workgroups on 256 CUs the dispatcher otherwise packs two onto a CU
+  // (LDS and registers admit two) and leaves others idle; dynamic LDS past half the CU's 160 KB prevents it
+  constexpr size_t kStatic = 2 * sizeof(float) * (size_t)(kProjRows + 2 * ((NT + 1) / 2) * 16) * kProjLd;
+  const size_t pad = R >= 64 * 256 ? 0 : (kStatic < 82 * 1024 ? 82 * 1024 - kStatic : 0);
+  hipLaunchKernelGGL(projections_kernel<NT>, grid, dim3(512), pad, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2,
                      n2, y, y_ld, R);
 }
 

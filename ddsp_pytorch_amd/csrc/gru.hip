@@ -154,6 +154,251 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------------------
+// The recurrence as ONE persistent launch (hidden 512, batch <= 64): the per-step launches above pay a
+// kernel boundary and re-stage their W_hh slice into LDS every step (7.4-7.8 us per step at config 2).
+// Batch items are independent, so the 256 workgroups (one per CU) form 8 groups of 32; group g owns items
+// g, g + 8, ... (<= 8 of them) and its slot s owns hidden units [16 s, 16 s + 16): the slot's 48 rows of
+// W_hh (gates r, z, n) stay in LDS for the whole sequence.  A step needs the group's whole h_{t-1},
+// written by its 32 slots: each slot stores its 16 units per item, drains them (s_waitcnt vmcnt(0)),
+// joins a workgroup barrier, and ONE lane adds to the group's counter (agent-scope atomic); a slot starts
+// step t once that counter reaches 32 t (one lane polls with sc1 loads, then a workgroup barrier) and
+// reads h_{t-1} with sc1 loads (L1 bypassed) — MI355X_MICROARCH.md "Valid forms", hand-off table row 1.
+// Where the groups live is decided at start by a census, not assumed: every workgroup reads its XCD
+// (HW_REG_XCC_ID), takes a ticket on that XCD's arrival counter, then waits until all 256 have arrived.
+//   * every XCD holds exactly 32 workgroups (the observed round-robin dispatch): group = XCD, slot =
+//     ticket, and h stays in that XCD's L2 — plain (write-back) stores, L2-served sc1 loads;
+//   * otherwise: group = blockIdx % 8, slot = blockIdx / 8, and h goes through memory — write-through
+//     (sc1) stores — so any placement is correct, only slower.
+// The h_t addresses are fresh every step (the output sequence), so no cache holds an older copy.  Every
+// wait is bounded: a launch whose workgroups cannot all be resident at once sets an abort word and ends
+// (garbage out) instead of hanging.  Per step a lane of wave w holds h[4 items][32 k of the wave's 64] in
+// registers and streams 3 rows x 32 k of the W slice from LDS (384 FMAs); the two k halves are summed by
+// one DPP rotation, the 8 waves through LDS, and 128 epilogue threads apply the gates, one (item, unit)
+// each.  (A 6-rows x 8-items x 8-k lane layout spent more VALU on its 3-level in-wave reduction than on
+// the FMAs: 2.9 us per step for the products against ~1 us now, tools/exp_gru_clock.py.)
+constexpr int kPG = 8;             // groups (items g, g + 8, ... belong to group g)
+constexpr int kPS = 32;            // slots per group
+constexpr int kPU = 16;            // hidden units per slot (hidden = kPS * kPU = 512)
+constexpr int kPH = kPS * kPU;
+constexpr int kPR = 3 * kPU;       // W_hh rows per slot
+constexpr int kPI = 8;             // items per group (batch <= kPG * kPI)
+constexpr int kPWld = kPH + 4;     // LDS row stride of the W slice: the 8 rows a lane octet reads spread over the banks
+constexpr int kPCounterStride = 32;  // uint32 words between counters (one 128-B line each)
+// sync words: [g * stride] step counter of group g; [(8 + x) * stride] arrivals on XCD x; [16 * stride] all
+// arrivals; [17 * stride] abort
+constexpr int kPSyncWords = 18 * kPCounterStride;
+constexpr uint64_t kPSpinTicks = 20000000;  // 200 ms at the 100 MHz realtime clock: an abort, never a hang
+
+__device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int voff) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 16 /* sc1 */);
+  return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
+}
+
+template <int AUX>
+__device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, int voff, float4 v) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 x = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, AUX);
+}
+
+// lane 0 waits until *word >= target (sc1 polls), bounded; false = aborted (by itself or another group)
+__device__ __forceinline__ bool wait_at_least(uint32_t* word, uint32_t target, uint32_t* abort_word) {
+  uint32_t n = 0;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if ((++n & 63) == 0 && (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                            __builtin_amdgcn_s_memrealtime() - t_start > kPSpinTicks)) {
+      __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+template <bool kLocal>
+__device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp, const float* __restrict__ b_hh,
+                                                    const float* __restrict__ h0, float* __restrict__ h_last,
+                                                    float* __restrict__ save, int B, int T, int g, int s,
+                                                    uint32_t* __restrict__ counter, uint32_t* __restrict__ abort_word,
+                                                    __amdgpu_buffer_rsrc_t rout, const float* Ws, float (*part)[kPR][kPI],
+                                                    int* s_abort) {
+  constexpr int kStoreAux = kLocal ? 0 : 16;  // write-back into the XCD's L2, or write-through (sc1)
+  const int nI = B > g ? (B - g + kPG - 1) / kPG : 0;  // items of this group
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  // lane -> 3 rows (row group rg of 16), 4 items (item group ig of 2), 32 k (k half ks of the wave's 64):
+  // ks sits on lane bit 3, so the pair sum over it is one DPP row rotation
+  const int rg = (l & 7) | (((l >> 4) & 1) << 3), ks = (l >> 3) & 1, ig = l >> 5;
+  const int kbase = 64 * w + 32 * ks;
+  const int64_t item_stride = (int64_t)T * kPH;  // floats between items in out
+  const int u0 = s * kPU;
+  // epilogue role: e < 128 -> unit u0 + eu of item ei
+  const int eu = tid & 15, ei = tid >> 4;
+  const bool epi = tid < kPU * kPI && ei < nI;
+  const int eb = g + kPG * ei;  // the epilogue item's batch index
+  float ebr = 0.f, ebz = 0.f, ebn = 0.f, ehp = 0.f;
+  if (epi) {
+    ebr = b_hh[u0 + eu];
+    ebz = b_hh[kPH + u0 + eu];
+    ebn = b_hh[2 * kPH + u0 + eu];
+    if (h0) ehp = h0[(int64_t)eb * kPH + u0 + eu];
+  }
+  for (int t = 0; t < T; ++t) {
+    // the epilogue's input projection for this step: issued before the wait
+    float exr = 0.f, exz = 0.f, exn = 0.f;
+    if (epi) {
+      const float* xr = xp + ((int64_t)eb * T + t) * 3 * kPH + u0 + eu;
+      exr = xr[0];
+      exz = xr[kPH];
+      exn = xr[2 * kPH];
+    }
+    if (t > 0) {  // every slot of the group has published h_{t-1}
+      if (tid == 0 && !wait_at_least(counter, (uint32_t)kPS * (uint32_t)t, abort_word)) *s_abort = 1;
+      __syncthreads();
+      if (*s_abort) return;
+    }
+    // h_{t-1}[4 ig + ii][kbase .. kbase + 32): all loads in flight before the first use
+    float4 hv[4][8];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int it = 4 * ig + ii;
+      const bool ok = it < nI;
+      const int bi = g + kPG * (ok ? it : 0);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t > 0)
+          v = ld_sc1_f4(rout, (int)(((int64_t)bi * item_stride + (int64_t)(t - 1) * kPH + kbase + 4 * c) * 4));
+        else if (h0)
+          v = *reinterpret_cast<const float4*>(h0 + (int64_t)bi * kPH + kbase + 4 * c);
+        hv[ii][c] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    float acc[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) acc[j][ii] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 wv = *reinterpret_cast<const float4*>(&Ws[(3 * rg + j) * kPWld + kbase + 4 * c]);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          float a = acc[j][ii];
+          a = fmaf(wv.x, hv[ii][c].x, a);
+          a = fmaf(wv.y, hv[ii][c].y, a);
+          a = fmaf(wv.z, hv[ii][c].z, a);
+          a = fmaf(wv.w, hv[ii][c].w, a);
+          acc[j][ii] = a;
+        }
+      }
+    }
+    // the wave's two k halves (lanes l, l ^ 8): one DPP row rotation; then the 8 waves through LDS
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+        acc[j][ii] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[j][ii]), 0x128, 0xF, 0xF, true));
+    if (ks == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        *reinterpret_cast<float4*>(&part[w][3 * rg + j][4 * ig]) = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+    __syncthreads();
+    if (epi) {
+      float hr = 0.f, hz = 0.f, hn = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {  // fixed order
+        hr += part[v][eu][ei];
+        hz += part[v][kPU + eu][ei];
+        hn += part[v][2 * kPU + eu][ei];
+      }
+      const float r = sigmoidf_(exr + (hr + ebr));
+      const float z = sigmoidf_(exz + (hz + ebz));
+      const float hb = hn + ebn;
+      const float n = tanhf(exn + r * hb);
+      const float hnew = (1.0f - z) * n + z * ehp;
+      const int64_t oi = (int64_t)eb * item_stride + (int64_t)t * kPH + u0 + eu;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(hnew), rout, (int)(oi * 4), 0, kStoreAux);
+      if (save) {
+        const int64_t plane = (int64_t)B * T * kPH;
+        save[oi] = r;
+        save[plane + oi] = z;
+        save[2 * plane + oi] = n;
+        save[3 * plane + oi] = hb;
+      }
+      if (h_last && t == T - 1) h_last[(int64_t)eb * kPH + u0 + eu] = hnew;
+      ehp = hnew;
+    }
+    if (t + 1 < T) {  // publish h_t: drained stores, the workgroup's barrier, one agent-scope add
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* __restrict__ w, int n) {
+  for (int i = threadIdx.x; i < n; i += 256) w[i] = 0u;
+}
+
+__global__ void __launch_bounds__(512) gru_persistent_kernel(
+    const float* __restrict__ xp, const float* __restrict__ w_hh, const float* __restrict__ b_hh,
+    const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
+    int B, int T, uint32_t* __restrict__ sync) {
+  __shared__ __attribute__((aligned(16))) float Ws[kPR * kPWld];    // 99 KB: row rho = gate * 16 + unit
+  __shared__ __attribute__((aligned(16))) float part[8][kPR][kPI];  // per-wave k partials
+  __shared__ int s_abort, s_local, s_slot, s_group;
+  const int tid = threadIdx.x;
+  uint32_t* abort_word = sync + 17 * kPCounterStride;
+  // census: this workgroup's XCD and its ticket there, then every workgroup's arrival
+  if (tid == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const uint32_t ticket = __hip_atomic_fetch_add(sync + (kPG + xcc) * kPCounterStride, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    // (the ticket's value is used: the XCD add has completed before the total add)
+    __hip_atomic_fetch_add(sync + 16 * kPCounterStride, ticket < 0x7fffffffu ? 1u : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    int ok = wait_at_least(sync + 16 * kPCounterStride, (uint32_t)(kPG * kPS), abort_word);
+    int local = 1;
+    if (ok) {
+      for (int x = 0; x < kPG; ++x)
+        local &= __hip_atomic_load(sync + (kPG + x) * kPCounterStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (uint32_t)kPS;
+    }
+    s_abort = !ok;
+    s_local = local;
+    s_group = local ? (int)xcc : (int)(blockIdx.x % kPG);
+    s_slot = local ? (int)ticket : (int)(blockIdx.x / kPG);
+  }
+  __syncthreads();
+  if (s_abort) return;
+  const int g = s_group, s = s_slot;
+  if (B <= g) return;  // the group has no items: nobody waits for it
+  const int u0 = s * kPU;
+  // this slot's W_hh rows into LDS, once
+  for (int f = tid; f < kPR * kPH / 4; f += 512) {
+    const int rho = f / (kPH / 4), k4 = f - rho * (kPH / 4);
+    const int gate = rho / kPU, u = rho - gate * kPU;
+    *reinterpret_cast<float4*>(&Ws[rho * kPWld + 4 * k4]) =
+        *reinterpret_cast<const float4*>(w_hh + (int64_t)(gate * kPH + u0 + u) * kPH + 4 * k4);
+  }
+  __syncthreads();
+  // out as a buffer resource: byte offsets (< 2^31, checked by the host) with cache-policy bits
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, 0x00020000);
+  uint32_t* counter = sync + g * kPCounterStride;
+  if (s_local)
+    gru_persistent_body<true>(xp, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, Ws, part, &s_abort);
+  else
+    gru_persistent_body<false>(xp, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, Ws, part, &s_abort);
+}
+
+// ---------------------------------------------------------------------------------------
 // Backward (BPTT) of the recurrence, for training.  With dh the total gradient reaching h_t:
 //   dn = dh (1 - z), dz = dh (h_{t-1} - n), da_n = dn (1 - n^2), da_z = dz z (1 - z),
 //   da_r = da_n hn r (1 - r), dhn = da_n r     (hn = W_hn h_{t-1} + b_hn)
@@ -454,6 +699,39 @@ static int gru_forward_launch(const float* xp, const float* w_hh, const float* b
 }
 
 extern "C" {
+
+size_t ddsp_hip_gru_persistent_workspace_size(void) { return sizeof(uint32_t) * kPSyncWords; }
+
+int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
+                                    float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || steps == 0) return DDSP_HIP_OK;
+  if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
+  if (hidden != kPH || batch > kPG * kPI || batch * steps * hidden * (int64_t)sizeof(float) >= ((int64_t)1 << 31) ||
+      steps > (int64_t)INT32_MAX / kPS)
+    return DDSP_HIP_ERANGE;
+  if (!workspace || workspace_bytes < ddsp_hip_gru_persistent_workspace_size()) return DDSP_HIP_EWORKSPACE;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(xp) | reinterpret_cast<uintptr_t>(w_hh) |
+                       reinterpret_cast<uintptr_t>(b_hh) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(h0) | reinterpret_cast<uintptr_t>(h_last) |
+                       reinterpret_cast<uintptr_t>(gates);
+  if (al & 15) return DDSP_HIP_ERANGE;
+  // every workgroup of a group must be resident at once (one 110 KB-LDS workgroup per CU)
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return DDSP_HIP_ELAUNCH;
+  if (cus < kPG * kPS) return DDSP_HIP_ERANGE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the sync words are zeroed by a kernel of ours: a hipMemsetAsync captured into a HIP graph wrote
+  // 0x5EE0B080 instead of 0 on every replay after the first (ROCm 7.2, tools/dbg_gru_graph.py)
+  hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, reinterpret_cast<uint32_t*>(workspace), kPSyncWords);
+  if (int r = launch_status()) return r;
+  hipLaunchKernelGGL(gru_persistent_kernel, dim3(kPG * kPS), dim3(512), 0, st, xp, w_hh, b_hh, h0, out, h_last, gates,
+                     (int)batch, (int)steps, reinterpret_cast<uint32_t*>(workspace));
+  return launch_status();
+}
 
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                          float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream) {

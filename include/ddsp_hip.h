@@ -281,6 +281,18 @@ int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, cons
  * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace: *_workspace_size. */
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                          float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream);
+/* The same forward as ONE persistent launch (hidden 512, batch <= 64, out < 2 GiB, >= 256 CUs; else
+ * DDSP_HIP_ERANGE and the caller uses ddsp_hip_gru_forward): 8 groups of 32 workgroups, group g owning
+ * items g, g + 8, ...; each workgroup keeps its 48 rows of W_hh in LDS for the whole sequence and the
+ * group's slots hand h_t to each other through the output sequence (write-through stores, a per-group
+ * counter).  Needs all 256 workgroups resident together (one per CU): launched on a stream whose kernels
+ * cannot reach every CU, it ends after a bounded wait with garbage output rather than hang.  Workspace:
+ * ddsp_hip_gru_persistent_workspace_size() bytes (zeroed by the call, on the stream, by a kernel of its own:
+ * the call stays capturable into a HIP graph). */
+size_t ddsp_hip_gru_persistent_workspace_size(void);
+int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
+                                    float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden,
+                                    void* workspace, size_t workspace_bytes, void* stream);
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden);
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,

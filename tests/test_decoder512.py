@@ -9,7 +9,7 @@ Goldens (tests/golden/make_goldens.py, run against /root/reference):
 Each stores the state_dict as per-tensor CRC32s: the tests rebuild this package's modules under the same
 seed (their constructors draw in the reference's order) and check every CRC before using them.
 
-At hidden 512 the GPU forward takes the shipped network kernels — the H=512 GRU step kernel, the 512-wide
+At hidden 512 the GPU forward takes the shipped network kernels — the H=512 persistent GRU recurrence, the 512-wide
 MLP blocks (LayerNorm + LeakyReLU epilogue, out_mlp's extras), the one-feature LayerNorm blocks, the
 projection GEMM — and the fused synthesis launch; the tests assert each route was taken (a spy on the
 C-ABI entry points called).  g5 / g9 (hidden 32) never reach those kernels.
@@ -127,9 +127,9 @@ def _check_outputs(o, g, batch):
 
 def _assert_network_routes(spy, n_gru_inputs):
     names = spy.names()
-    gru = [a for n, a in spy.calls if n == "gru_forward"]
-    assert gru and all(int(a[-2]) == 512 for a in gru), "the H=512 GRU step kernel did not run"
-    assert len(gru) == n_gru_inputs
+    gru = [a for n, a in spy.calls if n == "gru_forward_persistent"]  # hidden 512: the persistent recurrence
+    assert gru and all(int(a[9]) == 512 for a in gru), "the H=512 GRU kernel did not run"
+    assert len(gru) == n_gru_inputs and "gru_forward" not in names
     # f0_mlp / loudness_mlp blocks 2-3 and out_mlp's three blocks (+ z_mlp's) on the matrix-core block kernel
     assert spy.count("mlp_block") >= 7, names
     assert spy.count("layer_norm_leaky_relu") >= 2, names  # the one-feature first blocks
@@ -223,7 +223,7 @@ def test_g6b_decoder512_gradients_gpu(monkeypatch):
     w = torch.as_tensor(g["weight"]).cuda()
     (o["signal"] * w).sum().backward()
     torch.cuda.synchronize()
-    assert spy.count("gru_backward") == 1 and spy.count("gru_forward") == 1, spy.names()
+    assert spy.count("gru_backward") == 1 and spy.count("gru_forward_persistent") == 1, spy.names()
     errs = {"signal": rms(o["signal"].detach().cpu().numpy(), g["signal"])}
     assert errs["signal"] < PARITY_RMS, errs
 

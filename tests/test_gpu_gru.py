@@ -93,3 +93,34 @@ def test_gru_backward(dd, B, T, I, H, with_h0):
         assert relerr(p.grad, ref[n]) < 1e-5, (n, relerr(p.grad, ref[n]))
     if with_h0:
         assert relerr(h0g.grad, h0c.grad) < 1e-5, relerr(h0g.grad, h0c.grad)
+
+
+@pytest.mark.parametrize("B,T,with_h0", [(64, 200, False), (65, 3, False), (9, 31, True), (1, 1, True)])
+def test_gru_persistent_route(dd, monkeypatch, B, T, with_h0):
+    """Hidden 512 and batch <= 64: ONE persistent launch (ddsp_hip_gru_forward_persistent) runs the whole
+    recurrence; batch 65 answers ERANGE and takes the step kernels; both match torch's CPU GRU, and
+    repeated calls (the hand-off counters are re-zeroed per call) give identical results."""
+    calls = []
+    real = dd._lib.call
+
+    def spy(name, *a, **k):
+        st = real(name, *a, **k)
+        calls.append((name, st))
+        return st
+    monkeypatch.setattr(dd._lib, "call", spy)
+    torch.manual_seed(B + T)
+    g = torch.nn.GRU(1024, 512, batch_first=True)
+    x = torch.randn(B, T, 1024)
+    h0 = torch.randn(1, B, 512) * 0.5 if with_h0 else None
+    with torch.no_grad():
+        ref_out, ref_h = g(x, h0) if with_h0 else g(x)
+        gg = g.cuda()
+        outs = [dd.core.gru(x.cuda(), gg, h0.cuda() if with_h0 else None) for _ in range(3)]
+    torch.cuda.synchronize()
+    persistent = [st for n, st in calls if n == "gru_forward_persistent"]
+    assert persistent == ([0] * 3 if B <= 64 else [dd.core.ERANGE] * 3), calls
+    assert sum(n == "gru_forward" for n, _ in calls) == (0 if B <= 64 else 3)
+    for out, h in outs:
+        assert relerr(out, ref_out) < 1e-5, relerr(out, ref_out)
+        assert relerr(h, ref_h) < 1e-5
+        assert torch.equal(out, outs[0][0]) and torch.equal(h, outs[0][1])

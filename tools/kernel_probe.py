@@ -28,6 +28,19 @@ def main():
             out.backward(g, retain_graph=True)
         torch.cuda.synchronize()
         return
+    if which in ("proj", "mlp"):  # the decoder's projections (one launch) / one 512-wide MLP block
+        torch.manual_seed(0)
+        h = torch.randn(B * F, 512, device=dev)
+        l1, l2 = torch.nn.Linear(512, H + 1).to(dev), torch.nn.Linear(512, NB).to(dev)
+        lin, ln, act = torch.nn.Linear(512, 512).to(dev), torch.nn.LayerNorm(512).to(dev), torch.nn.LeakyReLU()
+        with torch.no_grad():
+            for _ in range(reps):
+                if which == "proj":
+                    core.projections(h, l1, l2)
+                else:
+                    core.mlp_block(h, lin, ln, act)
+        torch.cuda.synchronize()
+        return
     if which == "gru":  # the decoder's GRU recurrence (B=64, T=200, hidden 512): step kernels
         torch.manual_seed(0)
         g = torch.nn.GRU(1024, 512, batch_first=True).to(dev)
