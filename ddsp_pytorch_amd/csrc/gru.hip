@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
 // kernel boundary and re-stage their W_hh slice into LDS every step (7.4-7.8 us per step at config 2).
 // Batch items are independent, so the 256 workgroups (one per CU) form 8 groups of 32; group g owns items
 // g, g + 8, ... (<= 8 of them) and its slot s owns hidden units [16 s, 16 s + 16): the slot's 48 rows of
-// W_hh (gates r, z, n) stay in LDS for the whole sequence.  A step needs the group's whole h_{t-1},
+// W_hh (gates r, z, n) stay on-chip for the whole sequence.  A step needs the group's whole h_{t-1},
 // written by its 32 slots: each slot stores its 16 units per item, drains them (s_waitcnt vmcnt(0)),
 // joins a workgroup barrier, and ONE lane adds to the group's counter (agent-scope atomic); a slot starts
 // step t once that counter reaches 32 t (one lane polls with sc1 loads, then a workgroup barrier) and
@@ -171,18 +171,20 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
 //     (sc1) stores — so any placement is correct, only slower.
 // The h_t addresses are fresh every step (the output sequence), so no cache holds an older copy.  Every
 // wait is bounded: a launch whose workgroups cannot all be resident at once sets an abort word and ends
-// (garbage out) instead of hanging.  Per step a lane of wave w holds h[4 items][32 k of the wave's 64] in
-// registers and streams 3 rows x 32 k of the W slice from LDS (384 FMAs); the two k halves are summed by
-// one DPP rotation, the 8 waves through LDS, and 128 epilogue threads apply the gates, one (item, unit)
-// each.  (A 6-rows x 8-items x 8-k lane layout spent more VALU on its 3-level in-wave reduction than on
-// the FMAs: 2.9 us per step for the products against ~1 us now, tools/exp_gru_clock.py.)
+// (garbage out) instead of hanging.  The slot's 48 rows of W_hh (gates r, z, n of its 16 units) live in
+// REGISTERS for the whole sequence: lane l of wave w holds rows 6 (l >> 3) .. + 5 at k = 64 w + 8 (l & 7)
+// .. + 7 (48 values).  Per step h_{t-1} of the group's items is staged once into LDS (16 KB), each lane
+// reads its 8 k of all 8 items (384 FMAs), the 8 k octets of a row group are summed in a DPP half-row,
+// the 8 waves through LDS, and 128 epilogue threads apply the gates, one (item, unit) each.  (Per-step
+// phases by in-kernel stamps, tools/exp_gru_clock.py: W streamed from LDS and h loaded per lane from L2,
+// the lanes' operand traffic — 128-256 KB per CU per step through the 64 B/clk load path — cost 2.9-3.4
+// us of a 4.8-5.0 us step.)
 constexpr int kPG = 8;             // groups (items g, g + 8, ... belong to group g)
 constexpr int kPS = 32;            // slots per group
 constexpr int kPU = 16;            // hidden units per slot (hidden = kPS * kPU = 512)
 constexpr int kPH = kPS * kPU;
 constexpr int kPR = 3 * kPU;       // W_hh rows per slot
 constexpr int kPI = 8;             // items per group (batch <= kPG * kPI)
-constexpr int kPWld = kPH + 4;     // LDS row stride of the W slice: the 8 rows a lane octet reads spread over the banks
 constexpr int kPCounterStride = 32;  // uint32 words between counters (one 128-B line each)
 // sync words: [g * stride] step counter of group g; [(8 + x) * stride] arrivals on XCD x; [16 * stride] all
 // arrivals; [17 * stride] abort
@@ -217,22 +219,40 @@ __device__ __forceinline__ bool wait_at_least(uint32_t* word, uint32_t target, u
   return true;
 }
 
+// sum over the 8 lanes l & ~7 .. l | 7 (a DPP half-row), in every lane: VALU only
+__device__ __forceinline__ float dpp_sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  return v;
+}
+
 template <bool kLocal>
-__device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp, const float* __restrict__ b_hh,
-                                                    const float* __restrict__ h0, float* __restrict__ h_last,
-                                                    float* __restrict__ save, int B, int T, int g, int s,
-                                                    uint32_t* __restrict__ counter, uint32_t* __restrict__ abort_word,
-                                                    __amdgpu_buffer_rsrc_t rout, const float* Ws, float (*part)[kPR][kPI],
-                                                    int* s_abort) {
+__device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp, const float* __restrict__ w_hh,
+                                                    const float* __restrict__ b_hh, const float* __restrict__ h0,
+                                                    float* __restrict__ h_last, float* __restrict__ save, int B, int T,
+                                                    int g, int s, uint32_t* __restrict__ counter,
+                                                    uint32_t* __restrict__ abort_word, __amdgpu_buffer_rsrc_t rout,
+                                                    float* hs, float (*part)[kPR][kPI], int* s_abort) {
   constexpr int kStoreAux = kLocal ? 0 : 16;  // write-back into the XCD's L2, or write-through (sc1)
   const int nI = B > g ? (B - g + kPG - 1) / kPG : 0;  // items of this group
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  // lane -> 3 rows (row group rg of 16), 4 items (item group ig of 2), 32 k (k half ks of the wave's 64):
-  // ks sits on lane bit 3, so the pair sum over it is one DPP row rotation
-  const int rg = (l & 7) | (((l >> 4) & 1) << 3), ks = (l >> 3) & 1, ig = l >> 5;
-  const int kbase = 64 * w + 32 * ks;
+  // lane -> 6 rows (row group rg of 8: rows 6 rg .. 6 rg + 5, row rho = gate * 16 + unit) x 8 k (k octet
+  // ks of the wave's 64); the 8 lanes of one row group are contiguous, so its k partials sum in a DPP half-row
+  const int ks = l & 7, rg = l >> 3;
+  const int kbase = 64 * w + 8 * ks;
   const int64_t item_stride = (int64_t)T * kPH;  // floats between items in out
   const int u0 = s * kPU;
+  // this lane's 48 weights of the slot's W_hh rows, in registers for the whole sequence
+  float wr[6][8];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int rho = 6 * rg + j, gate = rho / kPU, u = rho - gate * kPU;
+    const float* src = w_hh + (int64_t)(gate * kPH + u0 + u) * kPH + kbase;
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    wr[j][0] = a.x; wr[j][1] = a.y; wr[j][2] = a.z; wr[j][3] = a.w;
+    wr[j][4] = b.x; wr[j][5] = b.y; wr[j][6] = b.z; wr[j][7] = b.w;
+  }
   // epilogue role: e < 128 -> unit u0 + eu of item ei
   const int eu = tid & 15, ei = tid >> 4;
   const bool epi = tid < kPU * kPI && ei < nI;
@@ -244,6 +264,10 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
     ebn = b_hh[2 * kPH + u0 + eu];
     if (h0) ehp = h0[(int64_t)eb * kPH + u0 + eu];
   }
+  // h staging role: thread -> item tid >> 6, floats 8 (tid & 63) .. + 7 of its 512
+  const int hi = tid >> 6, hk = 8 * (tid & 63);
+  const bool hok = hi < nI;
+  const int hb = g + kPG * (hok ? hi : 0);
   for (int t = 0; t < T; ++t) {
     // the epilogue's input projection for this step: issued before the wait
     float exr = 0.f, exz = 0.f, exn = 0.f;
@@ -258,68 +282,65 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
       __syncthreads();
       if (*s_abort) return;
     }
-    // h_{t-1}[4 ig + ii][kbase .. kbase + 32): all loads in flight before the first use
-    float4 hv[4][8];
+    // h_{t-1} of the group's items into LDS, once per step (zeros past nI)
+    {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (t > 0) {
+        const int off = (int)(((int64_t)hb * item_stride + (int64_t)(t - 1) * kPH + hk) * 4);
+        a = ld_sc1_f4(rout, off);
+        b = ld_sc1_f4(rout, off + 16);
+      } else if (h0) {
+        a = *reinterpret_cast<const float4*>(h0 + (int64_t)hb * kPH + hk);
+        b = *reinterpret_cast<const float4*>(h0 + (int64_t)hb * kPH + hk + 4);
+      }
+      if (!hok) a = b = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&hs[hi * kPH + hk]) = a;
+      *reinterpret_cast<float4*>(&hs[hi * kPH + hk + 4]) = b;
+    }
+    __syncthreads();
+    float acc[6][kPI];
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int it = 4 * ig + ii;
-      const bool ok = it < nI;
-      const int bi = g + kPG * (ok ? it : 0);
+    for (int i = 0; i < kPI; ++i) {
+      const float4 ha = *reinterpret_cast<const float4*>(&hs[i * kPH + kbase]);
+      const float4 hb4 = *reinterpret_cast<const float4*>(&hs[i * kPH + kbase + 4]);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (t > 0)
-          v = ld_sc1_f4(rout, (int)(((int64_t)bi * item_stride + (int64_t)(t - 1) * kPH + kbase + 4 * c) * 4));
-        else if (h0)
-          v = *reinterpret_cast<const float4*>(h0 + (int64_t)bi * kPH + kbase + 4 * c);
-        hv[ii][c] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = 0; j < 6; ++j) {
+        float v = wr[j][0] * ha.x;
+        v = fmaf(wr[j][1], ha.y, v);
+        v = fmaf(wr[j][2], ha.z, v);
+        v = fmaf(wr[j][3], ha.w, v);
+        v = fmaf(wr[j][4], hb4.x, v);
+        v = fmaf(wr[j][5], hb4.y, v);
+        v = fmaf(wr[j][6], hb4.z, v);
+        v = fmaf(wr[j][7], hb4.w, v);
+        acc[j][i] = v;
       }
     }
-    float acc[3][4];
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 6; ++j)
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) acc[j][ii] = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const float4 wv = *reinterpret_cast<const float4*>(&Ws[(3 * rg + j) * kPWld + kbase + 4 * c]);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          float a = acc[j][ii];
-          a = fmaf(wv.x, hv[ii][c].x, a);
-          a = fmaf(wv.y, hv[ii][c].y, a);
-          a = fmaf(wv.z, hv[ii][c].z, a);
-          a = fmaf(wv.w, hv[ii][c].w, a);
-          acc[j][ii] = a;
-        }
-      }
-    }
-    // the wave's two k halves (lanes l, l ^ 8): one DPP row rotation; then the 8 waves through LDS
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-        acc[j][ii] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[j][ii]), 0x128, 0xF, 0xF, true));
+      for (int i = 0; i < kPI; ++i) acc[j][i] = dpp_sum8(acc[j][i]);  // over the wave's 8 k octets
     if (ks == 0) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        *reinterpret_cast<float4*>(&part[w][3 * rg + j][4 * ig]) = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int i = 0; i < kPI; i += 4)
+          *reinterpret_cast<float4*>(&part[w][6 * rg + j][i]) =
+              make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);
     }
     __syncthreads();
     if (epi) {
       float hr = 0.f, hz = 0.f, hn = 0.f;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {  // fixed order
+      for (int v = 0; v < 8; ++v) {  // over the 8 waves, fixed order
         hr += part[v][eu][ei];
         hz += part[v][kPU + eu][ei];
         hn += part[v][2 * kPU + eu][ei];
       }
       const float r = sigmoidf_(exr + (hr + ebr));
       const float z = sigmoidf_(exz + (hz + ebz));
-      const float hb = hn + ebn;
-      const float n = tanhf(exn + r * hb);
+      const float hbn = hn + ebn;
+      const float n = tanhf(exn + r * hbn);
       const float hnew = (1.0f - z) * n + z * ehp;
       const int64_t oi = (int64_t)eb * item_stride + (int64_t)t * kPH + u0 + eu;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(hnew), rout, (int)(oi * 4), 0, kStoreAux);
@@ -328,7 +349,7 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
         save[oi] = r;
         save[plane + oi] = z;
         save[2 * plane + oi] = n;
-        save[3 * plane + oi] = hb;
+        save[3 * plane + oi] = hbn;
       }
       if (h_last && t == T - 1) h_last[(int64_t)eb * kPH + u0 + eu] = hnew;
       ehp = hnew;
@@ -349,7 +370,7 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
     const float* __restrict__ xp, const float* __restrict__ w_hh, const float* __restrict__ b_hh,
     const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
     int B, int T, uint32_t* __restrict__ sync) {
-  __shared__ __attribute__((aligned(16))) float Ws[kPR * kPWld];    // 99 KB: row rho = gate * 16 + unit
+  __shared__ __attribute__((aligned(16))) float hs[kPI * kPH];      // h_{t-1} of the group's items, 16 KB
   __shared__ __attribute__((aligned(16))) float part[8][kPR][kPI];  // per-wave k partials
   __shared__ int s_abort, s_local, s_slot, s_group;
   const int tid = threadIdx.x;
@@ -380,22 +401,15 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
   if (s_abort) return;
   const int g = s_group, s = s_slot;
   if (B <= g) return;  // the group has no items: nobody waits for it
-  const int u0 = s * kPU;
-  // this slot's W_hh rows into LDS, once
-  for (int f = tid; f < kPR * kPH / 4; f += 512) {
-    const int rho = f / (kPH / 4), k4 = f - rho * (kPH / 4);
-    const int gate = rho / kPU, u = rho - gate * kPU;
-    *reinterpret_cast<float4*>(&Ws[rho * kPWld + 4 * k4]) =
-        *reinterpret_cast<const float4*>(w_hh + (int64_t)(gate * kPH + u0 + u) * kPH + 4 * k4);
-  }
-  __syncthreads();
   // out as a buffer resource: byte offsets (< 2^31, checked by the host) with cache-policy bits
   const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, 0x00020000);
   uint32_t* counter = sync + g * kPCounterStride;
   if (s_local)
-    gru_persistent_body<true>(xp, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, Ws, part, &s_abort);
+    gru_persistent_body<true>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
+                              &s_abort);
   else
-    gru_persistent_body<false>(xp, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, Ws, part, &s_abort);
+    gru_persistent_body<false>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
+                               &s_abort);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -25,8 +25,8 @@ PROBES = {
                ("    // the epilogue's input projection for this step: issued before the wait\n",
                 "    " + _STAMP.format(k=0) + "\n"),
                ("      if (*s_abort) return;\n    }\n", "      if (*s_abort) return;\n    }\n    " + _STAMP.format(k=1) + "\n"),
-               ("make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);\n    }\n    __syncthreads();\n",
-                "make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);\n    }\n    __syncthreads();\n    " + _STAMP.format(k=2) + "\n"),
+               ("make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);\n    }\n    __syncthreads();\n",
+                "make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);\n    }\n    __syncthreads();\n    " + _STAMP.format(k=2) + "\n"),
                ("      ehp = hnew;\n    }\n", "      ehp = hnew;\n    }\n    " + _STAMP.format(k=3) + "\n"),
                ("      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n",
                 "      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n      " + _STAMP.format(k=4) + "\n")],
