@@ -615,27 +615,20 @@ def mlp_block(x, linear, norm, act, out=None, extras=()):
     return None if st == ERANGE else out
 
 
-def projections(x, lin1, lin2):
-    """decoder.py:106-117: (lin1(x), lin2(x)) — harmonic_proj and noise_proj — as ONE launch reading both
-    nn.Linear layers' own parameters (ddsp_hip_projections: fp32 matrix cores).  The two results are
-    column slices of one [..., n1 + n2 (rounded up to 4)] buffer, which the fused synthesis kernel reads
-    with that row stride.  Returns None where the kernel does not apply (the caller runs torch's
-    Linear layers); inference only."""
+def projections(x, lin1, lin2, pad_to=64):
+    """decoder.py:106-117 as ONE library GEMM: both layers' parameters stacked, fresh every call, into a
+    zero-padded [n_pad, K] buffer (ddsp_hip_stack_rows, one launch; n_pad a multiple of ``pad_to``:
+    hipBLASLt runs 192 outputs in 28-30 us, the unpadded 166 in 38-39), then F.linear.  Returns the two
+    outputs as column slices of one [..., n_pad] result.  Nothing is cached on the modules."""
     _dev(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
     n1, n2, K = lin1.out_features, lin2.out_features, x.shape[-1]
-    if lin1.in_features != K or lin2.in_features != K:
-        raise RuntimeError(f"projections: input features {K} vs {lin1.in_features} / {lin2.in_features}")
-    xc = _c(x)
-    lead = tuple(x.shape[:-1])
-    rows = xc.numel() // K if K else 0
-    ld = -(-(n1 + n2) // 4) * 4
-    y = torch.empty(*lead, ld, dtype=torch.float32, device=x.device)
+    n_pad = -(-(n1 + n2) // pad_to) * pad_to
+    w = torch.empty(n_pad, K, dtype=torch.float32, device=x.device)
+    b = torch.empty(n_pad, dtype=torch.float32, device=x.device)
     w1, w2 = _c(lin1.weight), _c(lin2.weight)
-    st = _lib.call("projections", _lib.ptr(xc), K, K, _lib.ptr(w1), w1.stride(0), _lib.ptr(_c(lin1.bias)), n1,
-                   _lib.ptr(w2), w2.stride(0), _lib.ptr(_c(lin2.bias)), n2, _lib.ptr(y), ld, int(rows),
-                   _lib.stream_of(y), allow=(ERANGE,))
-    if st == ERANGE:
-        return None
+    _lib.call("stack_rows", _lib.ptr(w1), w1.stride(0), _lib.ptr(_c(lin1.bias)), n1, _lib.ptr(w2), w2.stride(0),
+              _lib.ptr(_c(lin2.bias)), n2, K, _lib.ptr(w), _lib.ptr(b), n_pad, _lib.stream_of(w))
+    y = torch.nn.functional.linear(x, w, b)  # (this package's matrix-core projection kernel ran 40-44 us)
     return y[..., :n1], y[..., n1:n1 + n2]
 
 

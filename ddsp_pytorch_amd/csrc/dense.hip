@@ -17,7 +17,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <utility>
 
 #include "common.h"
 
@@ -415,151 +414,17 @@ __global__ void __launch_bounds__(512) mlp_block_kernel(
     }
 }
 
-// decoder.py:106-117, the two projections after the decoder network as ONE launch that reads both
-// nn.Linear layers' own parameters: y[r][c] = b[c] + sum_k x[r][k] W[c][k], (W, b) = harmonic_proj's
-// for c < n1, noise_proj's for n1 <= c < n1 + n2.  Same staging as mlp_block_kernel (exact fp32
-// v_mfma_f32_16x16x4_f32, x and W through one LDS stage of K = 32, the next stage's operands in
-// registers under the current stage's MFMAs).  A workgroup owns 64 rows and all NT 16-column tiles;
-// wave w computes row tile w & 3 against half w >> 2 of the column tiles (one A fragment shared by up
-// to 8 B tiles per LDS read).  Columns past n1 + n2 are zero weights, never stored.
-constexpr int kProjRows = 64;
-constexpr int kProjKC = 32;  // K per LDS stage (two stages in LDS: one barrier per stage)
-constexpr int kProjLd = kProjKC + 4;
-constexpr int kProjMaxTiles = 14;  // 224 columns (15 and 16 tiles spilled)
-
-template <int NT>
-__global__ void __launch_bounds__(512) projections_kernel(
-    const float* __restrict__ x, int64_t x_ld, int K, const float* __restrict__ w1, int64_t w1_ld,
-    const float* __restrict__ b1, int n1, const float* __restrict__ w2, int64_t w2_ld,
-    const float* __restrict__ b2, int n2, float* __restrict__ y, int64_t y_ld, int64_t R) {
-  constexpr int NA = (NT + 1) / 2;               // column tiles per wave (an odd NT pads one zero tile)
-  constexpr int NC = 2 * NA * 16;                // columns staged
-  constexpr int KV = kProjKC / 4;                 // float4s per row per stage
-  constexpr int NBL = (NC * KV + 511) / 512;     // W float4 loads per thread per stage
-  constexpr int NAL = kProjRows * KV / 512;      // x float4 loads per thread per stage
-  __shared__ __attribute__((aligned(16))) float As[2][kProjRows * kProjLd];
-  __shared__ __attribute__((aligned(16))) float Bs[2][NC * kProjLd];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int q = lane >> 4, l16 = lane & 15;
-  const int rt = wv & 3, tile0 = (wv >> 2) * NA;
-  const int64_t r0 = (int64_t)blockIdx.x * kProjRows;
-  const int nc = (K + kProjKC - 1) / kProjKC, ncol = n1 + n2;
-  // every load is unconditional from a valid address (clamped row / column / k) and zeroed by a
-  // select past the matrix: no divergent branches around the loads
-  const float* xr[NAL];
-#pragma unroll
-  for (int i = 0; i < NAL; ++i) {
-    const int arow = (t + 512 * i) / KV;
-    xr[i] = x + (r0 + arow < R ? r0 + arow : R - 1) * x_ld;
-  }
-  const float* wr[NBL];
-  bool wok[NBL];
-#pragma unroll
-  for (int i = 0; i < NBL; ++i) {
-    const int col = (t + 512 * i) / KV;
-    const int cc = col < ncol ? col : ncol - 1;
-    wr[i] = cc < n1 ? w1 + (int64_t)cc * w1_ld : w2 + (int64_t)(cc - n1) * w2_ld;
-    wok[i] = col < ncol;
-  }
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 sa[NAL], sb[NBL];
-  auto load = [&](int c) {
-    const int k = c * kProjKC + 4 * (t % KV);  // (512 * i) % KV == 0: the same k for every i
-    const int kk = k < K ? k : K - 4;
-#pragma unroll
-    for (int i = 0; i < NAL; ++i) {
-      sa[i] = *reinterpret_cast<const float4*>(xr[i] + kk);
-      if (k >= K) sa[i] = z4;
-    }
-#pragma unroll
-    for (int i = 0; i < NBL; ++i) {
-      sb[i] = *reinterpret_cast<const float4*>(wr[i] + kk);
-      if (!wok[i] || k >= K) sb[i] = z4;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NAL; ++i) {
-      const int f = t + 512 * i;
-      *reinterpret_cast<float4*>(&As[buf][(f / KV) * kProjLd + 4 * (f % KV)]) = sa[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NBL; ++i) {
-      const int f = t + 512 * i;
-      if (NBL * 512 == NC * KV || f < NC * KV)
-        *reinterpret_cast<float4*>(&Bs[buf][(f / KV) * kProjLd + 4 * (f % KV)]) = sb[i];
-    }
-  };
-  f32x4_t acc[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  // two LDS stages: stage c is read from buffer c & 1 while stage c + 1 is stored into the other one;
-  // the one barrier per stage (after that store) also ends every wave's reads of stage c - 1's buffer
-  load(0);
-  store(0);
-  __syncthreads();
-  if (nc > 1) load(1);
-  for (int c = 0; c < nc; ++c) {
-    const float* Ab = As[c & 1];
-    const float* Bb = Bs[c & 1];
-#pragma unroll
-    for (int h = 0; h < kProjKC / 16; ++h) {
-      const float4 af = *reinterpret_cast<const float4*>(&Ab[(16 * rt + l16) * kProjLd + 16 * h + 4 * q]);
-      float4 bf[NA];
-#pragma unroll
-      for (int j = 0; j < NA; ++j)
-        bf[j] = *reinterpret_cast<const float4*>(&Bb[(16 * (tile0 + j) + l16) * kProjLd + 16 * h + 4 * q]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float a = s == 0 ? af.x : s == 1 ? af.y : s == 2 ? af.z : af.w;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-          const float b = s == 0 ? bf[j].x : s == 1 ? bf[j].y : s == 2 ? bf[j].z : bf[j].w;
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
-        }
-      }
-    }
-    if (c + 1 < nc) {
-      store((c + 1) & 1);
-      __syncthreads();
-      if (c + 2 < nc) load(c + 2);  // lands under stage c + 1's MFMAs
-    }
-  }
-  // acc[j][e] is row 16 rt + 4 q + e, column 16 (tile0 + j) + l16
-#pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    const int col = 16 * (tile0 + j) + l16;
-    if (col >= ncol) continue;
-    const float bias = col < n1 ? b1[col] : b2[col - n1];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t row = r0 + 16 * rt + 4 * q + e;
-      if (row < R) y[row * y_ld + col] = acc[j][e] + bias;
-    }
-  }
-}
-
-template <int NT>
-void launch_projections(dim3 grid, hipStream_t st, const float* x, int64_t x_ld, int K, const float* w1,
-                        int64_t w1_ld, const float* b1, int n1, const float* w2, int64_t w2_ld, const float* b2,
-                        int n2, float* y, int64_t y_ld, int64_t R) {
-  // one workgroup per CU: with 200 workgroups on 256 CUs the dispatcher otherwise packs two onto a CU
-  // (LDS and registers admit two) and leaves others idle; dynamic LDS past half the CU's 160 KB prevents it
-  constexpr size_t kStatic = 2 * sizeof(float) * (size_t)(kProjRows + 2 * ((NT + 1) / 2) * 16) * kProjLd;
-  const size_t pad = R >= 64 * 256 ? 0 : (kStatic < 82 * 1024 ? 82 * 1024 - kStatic : 0);
-  hipLaunchKernelGGL(projections_kernel<NT>, grid, dim3(512), pad, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2,
-                     n2, y, y_ld, R);
-}
-
-template <int... NTs>
-void dispatch_projections(int nt, std::integer_sequence<int, NTs...>, dim3 grid, hipStream_t st, const float* x,
-                          int64_t x_ld, int K, const float* w1, int64_t w1_ld, const float* b1, int n1,
-                          const float* w2, int64_t w2_ld, const float* b2, int n2, float* y, int64_t y_ld,
-                          int64_t R) {
-  ((nt == NTs + 1 ? launch_projections<NTs + 1>(grid, st, x, x_ld, K, w1, w1_ld, b1, n1, w2, w2_ld, b2, n2, y, y_ld,
-                                                R)
-                  : void()),
-   ...);
+// The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
+// caller buffer): the GEMM that follows runs at a padded width hipBLASLt is fast at (28-30 us for 192
+// outputs against 38-39 us for the 166 of decoder.py:87-88 at config 2).  One launch, fresh every call.
+__global__ void __launch_bounds__(256) stack_rows_kernel(const float* __restrict__ w1, int64_t w1_ld, const float* __restrict__ b1,
+                                                         int n1, const float* __restrict__ w2, int64_t w2_ld,
+                                                         const float* __restrict__ b2, int n2, int K,
+                                                         float* __restrict__ w, float* __restrict__ b, int n_pad) {
+  const int r = blockIdx.x;
+  const float* src = r < n1 ? w1 + (int64_t)r * w1_ld : r < n1 + n2 ? w2 + (int64_t)(r - n1) * w2_ld : nullptr;
+  for (int k = threadIdx.x; k < K; k += 256) w[(int64_t)r * K + k] = src ? src[k] : 0.0f;
+  if (threadIdx.x == 0) b[r] = r < n1 ? b1[r] : r < n1 + n2 ? b2[r - n1] : 0.0f;
 }
 
 }  // namespace
@@ -648,23 +513,15 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
   return launch_status();
 }
 
-int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, const float* w1, int64_t w1_ld,
-                         const float* b1, int64_t n1, const float* w2, int64_t w2_ld, const float* b2, int64_t n2,
-                         float* y, int64_t y_ld, int64_t rows, void* stream) {
-  if (rows < 0 || in_features < 1 || n1 < 1 || n2 < 0 || !w1 || !b1 || (n2 > 0 && (!w2 || !b2)))
+int ddsp_hip_stack_rows(const float* w1, int64_t w1_ld, const float* b1, int64_t n1, const float* w2, int64_t w2_ld,
+                        const float* b2, int64_t n2, int64_t in_features, float* w, float* b, int64_t n_pad,
+                        void* stream) {
+  if (n1 < 1 || n2 < 0 || in_features < 1 || n_pad < n1 + n2 || !w1 || !b1 || !w || !b ||
+      (n2 > 0 && (!w2 || !b2)) || w1_ld < in_features || (n2 > 0 && w2_ld < in_features))
     return DDSP_HIP_EINVAL;
-  if (rows == 0) return DDSP_HIP_OK;
-  if (!x || !y || x_ld < in_features || w1_ld < in_features || (n2 > 0 && w2_ld < in_features) || y_ld < n1 + n2)
-    return DDSP_HIP_EINVAL;
-  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w1) |
-                       (n2 > 0 ? reinterpret_cast<uintptr_t>(w2) : 0);
-  if (n1 + n2 > 16 * kProjMaxTiles || in_features % 4 || in_features > INT32_MAX || (al & 15) || (x_ld & 3) || (w1_ld & 3) ||
-      (n2 > 0 && (w2_ld & 3)) || (rows + kProjRows - 1) / kProjRows > INT32_MAX)
-    return DDSP_HIP_ERANGE;  // callers keep torch's Linear
-  const int nt = (int)((n1 + n2 + 15) / 16);
-  const dim3 grid((unsigned)((rows + kProjRows - 1) / kProjRows));
-  dispatch_projections(nt, std::make_integer_sequence<int, kProjMaxTiles>{}, grid, reinterpret_cast<hipStream_t>(stream), x,
-                       x_ld, (int)in_features, w1, w1_ld, b1, (int)n1, w2, w2_ld, b2, (int)n2, y, y_ld, rows);
+  if (n_pad > INT32_MAX || in_features > INT32_MAX) return DDSP_HIP_ERANGE;
+  hipLaunchKernelGGL(stack_rows_kernel, dim3((unsigned)n_pad), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), w1,
+                     w1_ld, b1, (int)n1, w2, w2_ld, b2, (int)n2, (int)in_features, w, b, (int)n_pad);
   return launch_status();
 }
 

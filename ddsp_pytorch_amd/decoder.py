@@ -5,8 +5,8 @@ synth modules.
 The control network before the path runs at inference on gfx950 kernels
 too: each MLP block is one matrix-core launch with its LayerNorm + LeakyReLU (core.mlp_block), the
 GRU recurrence is the step kernel (core.gru; its input projection a hipBLASLt GEMM), the two
-projections one matrix-core launch over both layers' parameters (core.projections), and the synthesis
-section of ``forward``
+projections one hipBLASLt GEMM over both layers' parameters stacked per call (core.projections), and the
+synthesis section of ``forward``
 (decoder.py:106-125) one fused launch before the reverb.  Under autograd the MLPs and projections
 keep torch's modules; the GRU's BPTT runs on its backward step kernel.
 """
@@ -168,11 +168,11 @@ def _fp32_inference_ok(x, mods):
 
 
 def decoder_projections(self, hidden):
-    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden).  On the GPU at inference ONE
-    launch (core.projections: the fp32 matrix-core kernel reading both layers' own parameters — nothing
-    is copied, cached or rebound, so every write to a parameter, through ``.data`` included, is seen by
-    the next call); the two outputs are column slices of one buffer, which the fused synthesis kernel
-    reads with its row stride.  Under autograd the concatenated weights keep the call differentiable, so
+    """decoder.py:106-117: harmonic_proj(hidden), noise_proj(hidden).  On the GPU at inference ONE GEMM
+    (core.projections: both layers' parameters stacked fresh on every call into a zero-padded buffer, then
+    hipBLASLt — nothing is cached on or rebound in the modules, so every write to a parameter, through
+    ``.data`` included, is seen by the next call); the two outputs are column slices of one buffer, which
+    the fused synthesis kernel reads with its row stride.  Under autograd the concatenated weights keep the call differentiable, so
     the parameters receive their gradients as the reference's do."""
     hp, npj = self.harmonic_proj, self.noise_proj
     if not hidden.is_cuda or hp.bias is None or npj.bias is None or _hooked(hp) or _hooked(npj):

@@ -258,16 +258,13 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);
 
-/* decoder.py:106-117: param = harmonic_proj(hidden), magnitudes = noise_proj(hidden) as ONE launch over
- * the two nn.Linear layers' own parameters (no concatenated weight copy is kept or rebuilt):
- * y[r][c] = b1[c] + sum_k x[r][k] w1[c][k] for c < n1, b2[c-n1] + sum_k x[r][k] w2[c-n1][k] for
- * n1 <= c < n1 + n2; x [rows, x_ld], w1 [n1, w1_ld], w2 [n2, w2_ld], y [rows, y_ld] (y_ld >= n1 + n2:
- * param and magnitudes are its column slices, read by ddsp_hip_synth_frames_controls with that row
- * stride).  fp32 matrix cores (exact fp32 products and sums); n1 + n2 <= 224, K % 4 == 0 and 16-byte
- * aligned x / w rows, else DDSP_HIP_ERANGE (callers keep torch's Linear). */
-int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, const float* w1, int64_t w1_ld,
-                         const float* b1, int64_t n1, const float* w2, int64_t w2_ld, const float* b2, int64_t n2,
-                         float* y, int64_t y_ld, int64_t rows, void* stream);
+/* decoder.py:106-117 (param = harmonic_proj(hidden), magnitudes = noise_proj(hidden)): the two projections'
+ * parameters stacked into one zero-padded matrix w [n_pad, in_features] and
+ * bias b [n_pad] (caller buffers; rows n1 + n2 .. n_pad - 1 zero), for one library GEMM over both at a
+ * width it is fast at.  One launch; the parameters are read as they are at the call. */
+int ddsp_hip_stack_rows(const float* w1, int64_t w1_ld, const float* b1, int64_t n1, const float* w2, int64_t w2_ld,
+                        const float* b2, int64_t n2, int64_t in_features, float* w, float* b, int64_t n_pad,
+                        void* stream);
 
 /* ---------------- the decoder network's recurrence: decoder.py:33-68 (torch.nn.GRU) ----------------
  * out[B,T,H] = GRU(h0) over xp[B,T,3H] = x W_ih^T + b_ih (the input projection for every step,

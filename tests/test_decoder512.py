@@ -11,7 +11,7 @@ seed (their constructors draw in the reference's order) and check every CRC befo
 
 At hidden 512 the GPU forward takes the shipped network kernels — the H=512 persistent GRU recurrence, the 512-wide
 MLP blocks (LayerNorm + LeakyReLU epilogue, out_mlp's extras), the one-feature LayerNorm blocks, the
-projection GEMM — and the fused synthesis launch; the tests assert each route was taken (a spy on the
+projection GEMM over the stacked parameters — and the fused synthesis launch; the tests assert each route was taken (a spy on the
 C-ABI entry points called).  g5 / g9 (hidden 32) never reach those kernels.
 """
 import json
@@ -135,7 +135,7 @@ def _assert_network_routes(spy, n_gru_inputs):
     assert spy.count("layer_norm_leaky_relu") >= 2, names  # the one-feature first blocks
     assert any(int(a[1]) == 512 and a[6].value is not None for n, a in spy.calls if n == "mlp_block"), \
         "out_mlp's extras (f0, loudness) path did not run"
-    assert spy.count("projections") == 1, names  # both projections, one launch over their own parameters
+    assert spy.count("stack_rows") == 1, names  # both projections: one GEMM over their parameters stacked per call
     assert spy.count("synth_frames_controls") == 1, names
     assert spy.count("reverb_forward") == 1, names  # the device-validated IR cache + UPOLS
 
