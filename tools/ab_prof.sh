@@ -16,7 +16,7 @@ for rep in 1 2; do
     python3 - "$D/t_kernel_stats.csv" "$KERN" "$v" >> $ROOT/gpurun_out/ab_prof.log <<'EOF'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
-    if sys.argv[2] in r["Name"]:
+    if sys.argv[2] in r["Name"].replace(" ", ""):
         print(f"{sys.argv[3]:10s} {float(r['AverageNs']) / 1000:8.1f} us  (min {float(r['MinNs']) / 1000:.1f}, {r['Calls']} calls)")
 EOF
   done
