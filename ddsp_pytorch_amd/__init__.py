@@ -20,5 +20,6 @@ from .decoder import DDSPDecoder
 from .encoder import DDSPAutoencoder
 from .install import install
 from .modules import FilteredNoise, HarmonicSynth, Reverb
+from . import synth  # noqa: E402  (SynthPath, make_inputs: the bench's and the tests' synthesis-path driver)
 
 __version__ = "0.1.0"

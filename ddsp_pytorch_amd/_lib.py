@@ -63,6 +63,9 @@ SIGNATURES = {
                                    _I64, _F, _P]),
     "ddsp_hip_synth_frames_controls": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _P, _P, _P, _I64,
                                             _I64, _I64, _I64, _I64, _F, _P]),
+    "ddsp_hip_synth_frames_controls_prefix": (_I, [_P, _P, _I64, _P, _I64, _F, _P, _U64, _U64, _P, _P, _P, _P, _P,
+                                                   _I64, _I64, _I64, _I64, _I64, _F, _P]),
+    "ddsp_hip_frame_phase_prefix": (_I, [_P, _I64, _I64, _I64, _F, _P, _P]),
     "ddsp_hip_synth_frames_counter": (_I, [_P, _P, _P, _F, _U64, _P, _P, _I64, _I64, _I64, _I64, _I64, _F, _P]),
     "ddsp_hip_reverb_build_impulse": (_I, [_P, _P, _P, _P, _I64, _F, _P]),
     "ddsp_hip_reverb_spectrum_floats": (_SZ, [_I64, _I64]),

@@ -339,6 +339,9 @@ def _filtered_noise_launch(magnitudes, block_size, noise, add, return_noise, raw
 
 
 EWORKSPACE = 4  # DDSP_HIP_EWORKSPACE
+# the fused synthesis kernel's frames sum their phase prefix themselves up to this many frames per item
+# (O(F) per frame); past it one ddsp_hip_frame_phase_prefix launch precomputes every frame's prefix
+FRAME_PREFIX_MIN_FRAMES = 512
 ERANGE = 5
 
 
@@ -424,9 +427,14 @@ def _synth_frames_launch(f0, param, mags, block_size, sample_rate, bias, noise, 
     nz = torch.empty_like(out) if parts else None
     ctrl = (torch.empty(B * F * (1 + (H1 - 1) + NB), dtype=torch.float32, device=f0.device)
             if controls else None)
-    _lib.call("synth_frames_controls", _lib.ptr(f0c), _lib.ptr(pc), ldp, _lib.ptr(mc), ldm, float(bias),
-              _lib.ptr(noise), seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), _lib.ptr(ctrl), B, F,
-              H1 - 1, NB, bs, float(sample_rate), _lib.stream_of(out))
+    prefix = None
+    if F > FRAME_PREFIX_MIN_FRAMES:  # long renders: each frame reads its phase prefix instead of summing
+        prefix = torch.empty(B * F, dtype=torch.float64, device=f0.device)
+        _lib.call("frame_phase_prefix", _lib.ptr(f0c), B, F, bs, float(sample_rate), _lib.ptr(prefix),
+                  _lib.stream_of(out))
+    _lib.call("synth_frames_controls_prefix", _lib.ptr(f0c), _lib.ptr(pc), ldp, _lib.ptr(mc), ldm, float(bias),
+              _lib.ptr(noise), seed, offset, _lib.ptr(out), _lib.ptr(harm), _lib.ptr(nz), _lib.ptr(ctrl),
+              _lib.ptr(prefix), B, F, H1 - 1, NB, bs, float(sample_rate), _lib.stream_of(out))
     res = (out, harm, nz) if parts else out
     if not controls:
         return res

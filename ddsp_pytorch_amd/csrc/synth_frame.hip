@@ -52,7 +52,7 @@ __device__ __forceinline__ bool frame_synth(
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ ctrl_out, int B, int F, int H, int NB, int bs,
     float sr, int lo_end, int tail_start, int pad, int f, int b, int tid, int NT, float4* smem4, double* red,
-    int w0, float (&acc)[4], float (&nz)[4], int& j0_out, int ldp, int ldm) {
+    int w0, float (&acc)[4], float (&nz)[4], int& j0_out, int ldp, int ldm, const double* __restrict__ prefix) {
   const int n = 2 * (NB - 1), half = n >> 1, n4 = (n + 3) & ~3;
   const int H4 = (H + 3) & ~3;
   float2* coef = reinterpret_cast<float2*>(smem4);       // [H4] (k+1, amplitude)
@@ -72,7 +72,11 @@ __device__ __forceinline__ bool frame_synth(
 
   // ---- phase 1: independent loads and per-element work ----
   double part_s = 0.0, part_d = 0.0;
-  for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
+  if (prefix) {  // long renders: the item's exact frame prefix, precomputed (ddsp_hip_frame_phase_prefix)
+    if (tid == 0) part_s = prefix[frame];
+  } else {       // O(f) per frame: fine for the few hundred frames of a training / serving batch
+    for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
+  }
   // the frame's H + NB + 1 scale_function values as one work list (item i at thread i mod NT, in
   // ascending i, so the distribution's partial sums keep their order): harmonic distribution
   // (modules.py:53-60 before normalisation), noise magnitudes (modules.py:113), then the amplitude
@@ -306,14 +310,15 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
     const uint64_t* __restrict__ counter, float* __restrict__ out, float* __restrict__ harm_out,
     float* __restrict__ noise_out, float* __restrict__ ctrl_out, int F, int H,
-    int NB, int bs, float sr, int lo_end, int tail_start, int pad, int ldp, int ldm) {
+    int NB, int bs, float sr, int lo_end, int tail_start, int pad, int ldp, int ldm, const double* __restrict__ prefix) {
   extern __shared__ float4 smem4[];
   __shared__ double red[32];
   float acc[4], nz[4];
   int j0;
   if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
                                       (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
-                                      blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0, ldp, ldm))
+                                      blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0, ldp, ldm,
+                                      prefix))
     return;
   const int64_t o = ((int64_t)blockIdx.y * F + blockIdx.x) * bs + j0;
   if (harm_out) *reinterpret_cast<float4*>(harm_out + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -323,6 +328,36 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
 }
 
 __global__ void counter_advance_kernel(uint64_t* counter) { *counter += 1; }
+
+// frame_prefix[b * F + f] = sum_{g < f} bs * inc_g (exclusive), one workgroup per item: every thread sums a
+// contiguous run of frames, the runs' totals are scanned in LDS; every partial sum is an exact fp64 value
+// (the summands are fp32 increments scaled by bs, the span stays within 53 bits), so the order is free
+__global__ void __launch_bounds__(256) frame_prefix_kernel(const float* __restrict__ f0, int F, int bs, float sr,
+                                                           double* __restrict__ prefix) {
+  __shared__ double tot[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* f0b = f0 + (int64_t)b * F;
+  double* pb = prefix + (int64_t)b * F;
+  const int per = (F + 255) / 256, g0 = tid * per, g1 = min(g0 + per, F);
+  double run = 0.0;
+  for (int g = g0; g < g1; ++g) run += (double)bs * (double)phase_inc(f0b[g], sr);
+  tot[tid] = run;
+  __syncthreads();
+  if (tid == 0) {
+    double acc = 0.0;
+    for (int i = 0; i < 256; ++i) {
+      const double v = tot[i];
+      tot[i] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  double acc = tot[tid];
+  for (int g = g0; g < g1; ++g) {
+    pb[g] = acc;
+    acc += (double)bs * (double)phase_inc(f0b[g], sr);
+  }
+}
 
 }  // namespace
 }  // namespace ddsp
@@ -362,7 +397,8 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
                                const float* noise, uint64_t seed, uint64_t offset, uint64_t* counter, float* out,
                                float* harmonic_out, float* noise_out, float* controls_out, int64_t batch, int64_t frames,
                                int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
-                               void* stream, int64_t param_ld = -1, int64_t mags_ld = -1) {
+                               void* stream, int64_t param_ld = -1, int64_t mags_ld = -1,
+                               const double* prefix = nullptr) {
   if (param_ld < 0) param_ld = n_harmonic + 1;
   if (mags_ld < 0) mags_ld = n_bands;
   if (batch < 0 || frames < 0 || n_harmonic < 1 || n_bands < 2 || block_size < 4) return DDSP_HIP_EINVAL;
@@ -395,7 +431,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_, CTRL_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
                      bias, RNG_ ? nullptr : noise, k0, k1, o0, o1, RNG_ ? counter : nullptr, out, harmonic_out,  \
                      noise_out, controls_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, \
-                     tail_start, pad, (int)param_ld, (int)mags_ld)
+                     tail_start, pad, (int)param_ld, (int)mags_ld, prefix)
   if (noise) {
     if (G > 1) DDSP_SYNTH_FRAME_LAUNCH(false, true);
     else DDSP_SYNTH_FRAME_LAUNCH(false, false);
@@ -426,6 +462,29 @@ int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t 
   return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
                              noise_out, controls_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate,
                              stream, param_ld, magnitudes_ld);
+}
+
+int ddsp_hip_synth_frames_controls_prefix(const float* f0, const float* param, int64_t param_ld,
+                                          const float* raw_magnitudes, int64_t magnitudes_ld, float bias,
+                                          const float* noise, uint64_t seed, uint64_t offset, float* out,
+                                          float* harmonic_out, float* noise_out, float* controls_out,
+                                          const double* frame_prefix, int64_t batch, int64_t frames,
+                                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                                          void* stream) {
+  return synth_frames_launch(f0, param, raw_magnitudes, bias, noise, seed, offset, nullptr, out, harmonic_out,
+                             noise_out, controls_out, batch, frames, n_harmonic, n_bands, block_size, sample_rate,
+                             stream, param_ld, magnitudes_ld, frame_prefix);
+}
+
+int ddsp_hip_frame_phase_prefix(const float* f0, int64_t batch, int64_t frames, int64_t block_size, float sample_rate,
+                                double* frame_prefix, void* stream) {
+  if (batch < 0 || frames < 0 || block_size < 1 || !(sample_rate > 0)) return DDSP_HIP_EINVAL;
+  if (batch == 0 || frames == 0) return DDSP_HIP_OK;
+  if (!f0 || !frame_prefix) return DDSP_HIP_EINVAL;
+  if (batch > INT32_MAX || frames > INT32_MAX || block_size > INT32_MAX) return DDSP_HIP_ERANGE;
+  hipLaunchKernelGGL(frame_prefix_kernel, dim3((unsigned)batch), dim3(256), 0, S(stream), f0, (int)frames,
+                     (int)block_size, sample_rate, frame_prefix);
+  return launch_status();
 }
 
 int ddsp_hip_synth_frames_counter(const float* f0, const float* param, const float* raw_magnitudes, float bias,

@@ -153,6 +153,21 @@ int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t 
                                    uint64_t offset, float* out, float* harmonic_out, float* noise_out,
                                    float* controls_out, int64_t batch, int64_t frames, int64_t n_harmonic,
                                    int64_t n_bands, int64_t block_size, float sample_rate, void* stream);
+/* The same with frame_prefix (nullable): the exact fp64 phase prefix of every frame,
+ * frame_prefix[b * frames + f] = sum_{g < f} block_size * fl32(fl32(fl32(2 pi) f0[b, g]) / sr) (the
+ * reference's cumsum, core.py:138, at each frame's start), as ddsp_hip_frame_phase_prefix writes it.
+ * Without it every frame's workgroup sums its earlier frames itself: O(frames) per frame, O(frames^2)
+ * per item — the right choice for a few hundred frames, not for a minute of audio (5,625 frames at
+ * block 512).  Every partial sum is exact in fp64, so both give the same bits. */
+int ddsp_hip_synth_frames_controls_prefix(const float* f0, const float* param, int64_t param_ld,
+                                          const float* raw_magnitudes, int64_t magnitudes_ld, float bias,
+                                          const float* noise, uint64_t seed, uint64_t offset, float* out,
+                                          float* harmonic_out, float* noise_out, float* controls_out,
+                                          const double* frame_prefix, int64_t batch, int64_t frames,
+                                          int64_t n_harmonic, int64_t n_bands, int64_t block_size, float sample_rate,
+                                          void* stream);
+int ddsp_hip_frame_phase_prefix(const float* f0, int64_t batch, int64_t frames, int64_t block_size, float sample_rate,
+                                double* frame_prefix, void* stream);
 
 /* ddsp_hip_synth_frames for a stream of calls replayed from a captured HIP graph (the ddsp~
  * realtime host, realtime/ddsp_tilde/ddsp_model.cpp:32-52, calling the exported model once per
