@@ -188,19 +188,19 @@ __device__ __forceinline__ void ir_window(const float* __restrict__ noise, const
   }
 }
 
-// The reverb's forward transform (Z_b = FFT([x_b, 0]), grid rows y < npairs) with the IR cache's
-// validation in the same launch (row y = npairs, x = window): the MAC that follows reads a spectrum
-// that is current, and no launch is added to the step.  npairs == 0: the validation alone.
+// The reverb's forward transform (Z_b = FFT([x_b, 0]), grid rows y >= 1: pair y - 1) with the IR cache's
+// validation in the same launch (row y = 0, x = window — dispatched first, so the usually trivial
+// validation workgroups do not trail the transforms): the MAC that follows reads a spectrum that is
+// current, and no launch is added to the step.  npairs == 0: the validation alone.
 __global__ void __launch_bounds__(kNT) upols_forward_ir_kernel(
     const float* __restrict__ x, int64_t T, int rows, int nb, float2* __restrict__ X, const float* __restrict__ noise,
     const float* __restrict__ decay, const float* __restrict__ wet, int64_t klen, float sr, int force, int QG,
     float2* __restrict__ Hs, uint32_t* __restrict__ snap) {
   __shared__ float2 lds[kPad];
-  const int npairs = (int)gridDim.y - 1;
-  if ((int)blockIdx.y == npairs) {
+  if (blockIdx.y == 0) {
     if ((int)blockIdx.x < QG) ir_window(noise, decay, wet, klen, sr, force, blockIdx.x, Hs, snap, lds);
   } else if ((int)blockIdx.x < nb) {
-    forward_block(x, T, T, rows, 1, nb, 0, 2, 0, X, blockIdx.x, blockIdx.y, lds);
+    forward_block(x, T, T, rows, 1, nb, 0, 2, 0, X, blockIdx.x, blockIdx.y - 1, lds);
   }
 }
 
