@@ -136,7 +136,7 @@ def _assert_network_routes(spy, n_gru_inputs):
     assert any(int(a[1]) == 512 and a[6].value is not None for n, a in spy.calls if n == "mlp_block"), \
         "out_mlp's extras (f0, loudness) path did not run"
     assert spy.count("stack_rows") == 1, names  # both projections: one GEMM over their parameters stacked per call
-    assert spy.count("synth_frames_controls") == 1, names
+    assert spy.count("synth_frames_controls_prefix") == 1, names
     assert spy.count("reverb_forward") == 1, names  # the device-validated IR cache + UPOLS
 
 
