@@ -44,7 +44,7 @@ SIN_SLOTS = 4
 OSC_SLOTS_PER_SINE = 6 + SIN_SLOTS         # per (sample, harmonic): 6 fp32 VALU ops + one v_sin_f32
                                            # (synth_frame.hip inner loop; tools/loop_align.py counts it)
 
-DOMINANT_KERNEL = "synth_frame_kernelILb1ELb0ELb0EE"   # device noise, 4 samples/thread, no control dicts
+DOMINANT_KERNEL = "synth_frame_kernelILb1ELb0ELb0ELb0EE"   # device noise, 4 samples/thread, no control dicts
 
 
 def kernel_source_sha():

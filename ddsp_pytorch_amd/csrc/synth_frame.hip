@@ -45,8 +45,10 @@ __device__ __forceinline__ void osc_bank4(const float2* __restrict__ coef, int H
 // frame) acc = harmonic, nz = filtered noise.
 // PAD: one s_nop ahead of the (non-SPLIT) sine loop where an instantiation needs it for the loop's fast
 // placement (phase 5; the controls-writing instantiations).  CTRL: also write the frame's controls
-// (the dicts DDSPDecoder.forward returns) to ctrl_out.
-template <bool RNG, bool SPLIT, bool PAD, bool CTRL>
+// (the dicts DDSPDecoder.forward returns) to ctrl_out.  PREFIX: read the frame's phase prefix from
+// prefix[] (long renders) instead of summing the earlier frames; its own instantiations, so the
+// training / serving shapes run the code without the branch (1.9% of the kernel, same-box A/B).
+template <bool RNG, bool SPLIT, bool PAD, bool CTRL, bool PREFIX>
 __device__ __forceinline__ bool frame_synth(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
@@ -72,7 +74,7 @@ __device__ __forceinline__ bool frame_synth(
 
   // ---- phase 1: independent loads and per-element work ----
   double part_s = 0.0, part_d = 0.0;
-  if (prefix) {  // long renders: the item's exact frame prefix, precomputed (ddsp_hip_frame_phase_prefix)
+  if (PREFIX) {  // long renders: the item's exact frame prefix, precomputed (ddsp_hip_frame_phase_prefix)
     if (tid == 0) part_s = prefix[frame];
   } else {       // O(f) per frame: fine for the few hundred frames of a training / serving batch
     for (int g = tid; g < f; g += NT) part_s += (double)bs * (double)phase_inc(f0b[g], sr);
@@ -304,7 +306,7 @@ __device__ __forceinline__ bool frame_synth(
   return true;
 }
 
-template <bool RNG, bool SPLIT, bool CTRL>
+template <bool RNG, bool SPLIT, bool CTRL, bool PREFIX>
 __global__ void __launch_bounds__(256) synth_frame_kernel(
     const float* __restrict__ f0, const float* __restrict__ param, const float* __restrict__ mags,
     float bias, const float* __restrict__ noise, uint32_t k0, uint32_t k1, uint32_t off0, uint32_t off1,
@@ -315,7 +317,7 @@ __global__ void __launch_bounds__(256) synth_frame_kernel(
   __shared__ double red[32];
   float acc[4], nz[4];
   int j0;
-  if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
+  if (!frame_synth<RNG, SPLIT, /*PAD=*/CTRL, CTRL, PREFIX>(f0, param, mags, bias, noise, k0, k1, off0, off1, counter, ctrl_out,
                                       (int)gridDim.y, F, H, NB, bs, sr, lo_end, tail_start, pad, blockIdx.x,
                                       blockIdx.y, threadIdx.x, blockDim.x, smem4, red, 0, acc, nz, j0, ldp, ldm,
                                       prefix))
@@ -416,7 +418,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   if (sizeof(float) * floats > 120 * 1024) return DDSP_HIP_ERANGE;
   const int nt = std::max(64, ((bs / 4 + 63) / 64) * 64);
   // few frames (far fewer workgroups than CUs): split each frame's harmonics over G thread groups
-  int G = batch * frames < 512 ? std::max(1, std::min(4, 256 / nt)) : 1;
+  int G = batch * frames < 512 && !prefix ? std::max(1, std::min(4, 256 / nt)) : 1;
   if (sizeof(float) * (floats + (size_t)bs) > 120 * 1024) G = 1;
   const size_t shm = sizeof(float) * (floats + (G > 1 ? (size_t)bs : 0));
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -428,7 +430,12 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
     else DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, false);                                                  \
   } while (0)
 #define DDSP_SYNTH_FRAME_LAUNCH_(RNG_, SPLIT_, CTRL_)                                                      \
-  hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_, CTRL_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
+  do {                                                                                                  \
+    if (!SPLIT_ && prefix) DDSP_SYNTH_FRAME_LAUNCH_P(RNG_, false, CTRL_, true);                            \
+    else DDSP_SYNTH_FRAME_LAUNCH_P(RNG_, SPLIT_, CTRL_, false);                                            \
+  } while (0)
+#define DDSP_SYNTH_FRAME_LAUNCH_P(RNG_, SPLIT_, CTRL_, PREFIX_)                                            \
+  hipLaunchKernelGGL((synth_frame_kernel<RNG_, SPLIT_, CTRL_, PREFIX_>), grid, block, shm, S(stream), f0, param, raw_magnitudes, \
                      bias, RNG_ ? nullptr : noise, k0, k1, o0, o1, RNG_ ? counter : nullptr, out, harmonic_out,  \
                      noise_out, controls_out, (int)frames, (int)n_harmonic, (int)n_bands, bs, sample_rate, lo_end, \
                      tail_start, pad, (int)param_ld, (int)mags_ld, prefix)
@@ -441,6 +448,7 @@ static int synth_frames_launch(const float* f0, const float* param, const float*
   }
 #undef DDSP_SYNTH_FRAME_LAUNCH
 #undef DDSP_SYNTH_FRAME_LAUNCH_
+#undef DDSP_SYNTH_FRAME_LAUNCH_P
   if (!noise && counter) hipLaunchKernelGGL(counter_advance_kernel, dim3(1), dim3(1), 0, S(stream), counter);
   return launch_status();
 }

@@ -18,8 +18,8 @@ LIB = os.path.join(ROOT, "ddsp_pytorch_amd", "lib", "libddsp_hip.so")
 # kernel since the backward runs as two launches) and the frame-control harmonic backward.  The
 # one-sample-per-thread SPLIT forms run only for launches of few frames (the realtime stream),
 # which are latency-bound: reported, not pinned.
-PINNED = ("synth_frame_kernelILb1ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0EE",
-          "synth_frame_kernelILb1ELb0ELb1EE", "synth_frame_kernelILb0ELb0ELb1EE",
+PINNED = ("synth_frame_kernelILb1ELb0ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0ELb0EE",
+          "synth_frame_kernelILb1ELb0ELb1ELb0EE", "synth_frame_kernelILb0ELb0ELb1ELb0EE",
           "frame_backward_kernelILi2ELi0ELb0EE", "frame_backward_kernelILi1ELi0ELb0EE")
 
 

@@ -40,7 +40,7 @@ def kernel_instructions(so, kern):
     return ins
 
 
-def kernel_sha(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
+def kernel_sha(so, kern="synth_frame_kernelILb1ELb0ELb0ELb0EE"):
     """sha256 (16 hex) of one kernel's instruction stream (text and sizes, addresses relative to its
     entry): the key under which PMC counts of that kernel stay valid (bench.py, pmc_valu.py).  The
     literal of an s_add_u32 / s_addc_u32 (the PC-relative offset of a constant table after s_getpc_b64)
@@ -58,7 +58,7 @@ def kernel_sha(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
     return h.hexdigest()[:16]
 
 
-def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
+def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0ELb0EE"):
     """the kernel's sine loop: start address, size, 8-byte instructions at odd dword addresses"""
     ins = kernel_instructions(so, kern)
     # the hot loop: the innermost backward-branch loop holding >= 8 v_sin_f32
@@ -87,9 +87,9 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0EE"):
 
 # every shipped instantiation with a hardware-sine loop: fused forward (device noise / injected
 # noise, one sample per thread for few-frame launches), the harmonic-only fused backward
-SHIPPED = ("synth_frame_kernelILb1ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0EE",
-           "synth_frame_kernelILb1ELb1ELb0EE", "synth_frame_kernelILb0ELb1ELb0EE",
-           "synth_frame_kernelILb1ELb0ELb1EE", "synth_frame_kernelILb0ELb0ELb1EE",
+SHIPPED = ("synth_frame_kernelILb1ELb0ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0ELb0EE",
+           "synth_frame_kernelILb1ELb1ELb0ELb0EE", "synth_frame_kernelILb0ELb1ELb0ELb0EE",
+           "synth_frame_kernelILb1ELb0ELb1ELb0EE", "synth_frame_kernelILb0ELb0ELb1ELb0EE",
            "frame_backward_kernelILi2ELi2ELb1EE")
 
 
