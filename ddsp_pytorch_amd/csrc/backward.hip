@@ -40,9 +40,6 @@ __device__ __forceinline__ float scale_fn_grad(float x) {
   return 2.0f * kLn10F * p * one_minus;
 }
 
-// acc + g * sin(x) for |x| < kFastArgLimit.
-__device__ __forceinline__ float gsin_acc(float x, float g, float acc) { return fmaf(g, sin_reduced(x), acc); }
-
 // ---------------------------------------------------------------------------------------
 // scale_function backward: dx = g * scale_fn'(x + bias)
 __global__ void scale_backward_kernel(const float* __restrict__ x, const float* __restrict__ g,
@@ -119,7 +116,7 @@ constexpr int kKPT = 4;  // harmonics per thread
 
 // sine-loop placement padding per instantiation (tools/loop_align.py)
 template <int HMODE, int NOISE>
-constexpr bool kBwdLoopPad = true;
+constexpr bool kBwdLoopPad = false;
 
 template <int HMODE, int NOISE, bool RAW>
 __global__ void __launch_bounds__(512) frame_backward_kernel(
@@ -135,10 +132,14 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
   constexpr bool HARM = HMODE != 0;
   constexpr bool PARAMS = HMODE == 2;
   // LDS layout (mirrored by frame_backward_lds_floats): xl and gl start 16-B aligned
-  const int hfl = HARM ? 2 * bs + NS * H + H : 0;
+  // the NS sample segments are SL samples each (even, NS * SL >= bs; (omega, g) = 0 past bs adds exact
+  // zeros), so every thread's sine loop has the same scalar trip count: no per-lane exit masks (4 VALU per
+  // 8 sines before; 152 -> 146.5-147.7 us at config 2, same box, tools/ab_prof.sh bwd)
+  const int SL = ((bs + NS - 1) / NS + 1) & ~1, WGN = NS * SL;
+  const int hfl = HARM ? 2 * WGN + NS * H + H : 0;
   // (omega_t, g_t) per sample
-  float2* wg = reinterpret_cast<float2*>(smem);  // [bs]
-  float* part = smem + 2 * bs;                   // [NS * H]
+  float2* wg = reinterpret_cast<float2*>(smem);  // [WGN]
+  float* part = smem + 2 * WGN;                  // [NS * H]
   float* uk = part + NS * H;                     // [H] u_k (PARAMS: v_k first)
   const int n = NOISE ? 2 * (NB - 1) : 0, half = n >> 1;
   const int qmax = min(n, bs);
@@ -171,7 +172,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
         uk[k] = dist[frame * H + k];
       }
     }
-    for (int j = tid; j < bs; j += NT) wg[j].y = gf[j];
+    for (int j = tid; j < WGN; j += NT) wg[j].y = j < bs ? gf[j] : 0.0f;
   }
   if (NOISE) {
     for (int j = tid; j < bs + 8; j += NT) gl[j] = j < bs ? gf[j] : 0.0f;
@@ -198,7 +199,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
   float a = 0.0f;
   if (HARM) {
     const double dinc = (double)phase_inc(pitch0, sr);
-    for (int j = tid; j < bs; j += NT) wg[j].x = (float)(S0 + (double)(j + 1) * dinc);
+    for (int j = tid; j < WGN; j += NT) wg[j].x = j < bs ? (float)(S0 + (double)(j + 1) * dinc) : 0.0f;
     a = PARAMS ? scale_fn(prow[0]) : amp[frame];
     if (PARAMS)
       for (int k = tid; k < H; k += NT) uk[k] = uk[k] / norm;
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
     const int KQ = (H + kKPT - 1) / kKPT;
     for (int item = tid; item < KQ * NS; item += NTH) {
       const int s = item / KQ, kq = item - s * KQ;
-      const int j0 = (int)((int64_t)s * bs / NS), j1 = (int)((int64_t)(s + 1) * bs / NS);
+      const int j0 = s * SL, j1 = min(j0 + SL, bs);
       float kf[kKPT], acc[kKPT];
 #pragma unroll
       for (int c = 0; c < kKPT; ++c) {
@@ -234,14 +235,14 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
         float acc2[kKPT];
 #pragma unroll
         for (int c = 0; c < kKPT; ++c) acc2[c] = 0.0f;
-        int j = j0;
         // loop placement (tools/loop_align.py, pinned by tests/test_loop_align.py): the
         // 8-byte instructions at odd dword addresses; the alignment point makes the placement
         // independent of the code laid out before the loop, the s_nop flips it per instantiation
         if constexpr (kBwdLoopPad<HMODE, NOISE>) asm volatile(".p2align 3\n s_nop 0");
         else asm volatile(".p2align 3");
-        for (; j + 1 < j1; j += 2) {  // two samples per iteration: 8 independent sine chains
-          const float2 p = wg[j], p1 = wg[j + 1];
+        const float2* wq = wg + j0;
+        for (int i = 0; i < SL; i += 2) {  // two samples per iteration: 8 independent sine chains
+          const float2 p = wq[i], p1 = wq[i + 1];
           // the 8 chains written stage by stage so the scheduler keeps them interleaved (ILP 8)
           float y[2 * kKPT];
 #pragma unroll
@@ -254,11 +255,6 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
             acc[c] = fmaf(p.y, sin_rev(y[c]), acc[c]);
             acc2[c] = fmaf(p1.y, sin_rev(y[kKPT + c]), acc2[c]);
           }
-        }
-        if (j < j1) {
-          const float2 p = wg[j];
-#pragma unroll
-          for (int c = 0; c < kKPT; ++c) acc[c] = gsin_acc(p.x * kf[c], p.y, acc[c]);
         }
 #pragma unroll
         for (int c = 0; c < kKPT; ++c) acc[c] += acc2[c];
@@ -466,7 +462,8 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
 
 // LDS floats of frame_backward_kernel (its layout, written out on the host)
 size_t frame_backward_lds_floats(bool harm, bool noise, int H, int bs, int NS, int NB, int NSEG) {
-  const size_t hfl = harm ? (size_t)2 * bs + (size_t)NS * H + H : 0;
+  const size_t SL = (size_t)(((bs + NS - 1) / NS + 1) & ~1);
+  const size_t hfl = harm ? (size_t)2 * NS * SL + (size_t)NS * H + H : 0;
   if (!noise) return hfl;
   const int n = 2 * (NB - 1);
   const int qmax = std::min(n, bs);

@@ -348,6 +348,10 @@ __global__ void __launch_bounds__(kNT) upols_mac_ring_kernel(const float2* __res
     if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
 }
 
+// The adjoint MAC's whole-row form (upols_mac_adj_stream_kernel) for the row length it is built for:
+// 50 blocks (config 2's 102400 samples), up to 25 kernel windows (a 1 s IR at 48 kHz)
+constexpr int kStreamNB = 50, kStreamNQ = 25, kStreamPF = 4;
+
 // y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
 __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __restrict__ Y, int nb,
                                                             int64_t T, int rows, int pairing, int reverse,
@@ -494,6 +498,53 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* _
 #pragma unroll
   for (int d = 0; d < BLK; ++d)
     if (j0 + d < nb) Vp[(int64_t)(j0 + d) * kN] = make_float2(sgn * acc[d].x, sgn * acc[d].y);
+}
+
+// The adjoint sums for a whole pair row in one thread (nb == NBK, Q <= NQ): every GZ_m and H_q of the
+// bin is loaded once and stays in registers (the ring kernel's two chunks re-read ~1.5x of GZ), and the
+// outputs stream — step s issues the loads of step s + PF (GZ_{k-PF}, H_{s+PF}), then forms V_k,
+// k = NBK-1-s, from GZ_k..GZ_{k+s} and H_0..H_s already in registers and stores it, so loads, products
+// and stores overlap inside every wave (166 VGPRs; grid N/256 x npairs, one round at 2 waves/SIMD).
+// Config 2: 23.1-23.2 us against 29.8-29.9 for the ring kernel (same box, tools/ab_prof.sh reverb_bwd).
+// The same form of the forward MAC measured no faster than its ring kernel there (25.0 vs 24.9-25.0 us:
+// the forward ring's non-temporal loads already stream at ~4.9 TB/s), so the forward keeps the ring.
+template <int NBK, int NQ, int PF>
+__global__ void __launch_bounds__(kNT) upols_mac_adj_stream_kernel(const float2* __restrict__ G,
+                                                                   const float2* __restrict__ Hs, int nb, int Q,
+                                                                   float2* __restrict__ V) {
+  constexpr int kRow = kN * (int)sizeof(float2);
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int pair = blockIdx.y;
+  const float2* Grow = G + (int64_t)pair * nb * kN;
+  const int voff = f * (int)sizeof(float2);
+  float2 z[NBK], h[NQ];
+  auto zload = [&](int m) { z[m] = row_load<0>(Grow + (int64_t)m * kN, kRow, voff); };
+  auto hload = [&](int q) { h[q] = row_load<0>(Hs + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+#pragma unroll
+  for (int s = 0; s < PF; ++s) {
+    if (s < NQ) hload(s);
+    zload(NBK - 1 - s);
+  }
+  const float sgn = (f & 1) ? -1.0f : 1.0f;
+  float2* Vp = V + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int s = 0; s < NBK; ++s) {
+    const int k = NBK - 1 - s;
+    if (s + PF < NQ) hload(s + PF);
+    if (s + PF < NBK) zload(k - PF);
+    __builtin_amdgcn_sched_barrier(0);
+    v2f acc = {0.f, 0.f}, acc2 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q <= s) {
+        const float2 c = h[q];
+        if (q & 1) cmac(acc2, z[k + q], (v2f){c.x, -c.y}, (v2f){c.y, c.x});
+        else cmac(acc, z[k + q], (v2f){c.x, -c.y}, (v2f){c.y, c.x});
+      }
+    }
+    Vp[(int64_t)k * kN] = make_float2(sgn * (acc.x + acc2.x), sgn * (acc.y + acc2.y));
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 // dimp[pP + n] = Re(IFFT(sum_groups part[grp][p] + (-1)^f part[grp][p+1])) [P + n] / N for n < P,
@@ -685,9 +736,14 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   if (st) return st;
   if (dx) {
     constexpr int AB = kRingBlk;
-    hipLaunchKernelGGL((upols_mac_adj_ring_kernel<AB, kRingPF, kRingGR>),
-                       dim3(kN / kNT, (unsigned)((nb + AB - 1) / AB), (unsigned)npairs), dim3(kNT), 0, S(stream), GZ,
-                       reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
+    if (nb == kStreamNB && Q <= kStreamNQ)
+      hipLaunchKernelGGL((upols_mac_adj_stream_kernel<kStreamNB, kStreamNQ, kStreamPF>),
+                         dim3(kN / kNT, (unsigned)npairs), dim3(kNT), 0, S(stream), GZ,
+                         reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
+    else
+      hipLaunchKernelGGL((upols_mac_adj_ring_kernel<AB, kRingPF, kRingGR>),
+                         dim3(kN / kNT, (unsigned)((nb + AB - 1) / AB), (unsigned)npairs), dim3(kNT), 0, S(stream), GZ,
+                         reinterpret_cast<const float2*>(spectrum), (int)nb, (int)Q, V);
     if ((st = launch_status())) return st;
     hipLaunchKernelGGL(upols_inverse_kernel, dim3((unsigned)nb, (unsigned)npairs), dim3(kNT), 0, S(stream), V,
                        (int)nb, n, (int)rows, 1, 0, dx, n);

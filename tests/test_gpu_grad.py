@@ -230,7 +230,8 @@ def test_reverb_grad_golden(dd, tag):
 # (2, 102400, 96000): config 4's 48 kernel windows, more than one round of the adjoint MAC's
 # 27-slot register ring; (1, 131072, 120000): 60 windows, three rounds, and the IR correlation's
 # 25-lag kernel over three lag blocks
-@pytest.mark.parametrize("B,T,L", [(3, 102400, 48000), (2, 30000, 96000), (1, 2048, 2048),
+# (3, 102400, 48000) and (2, 102400, 30000): 50 blocks, the streaming adjoint MAC (all 25 / 16 windows)
+@pytest.mark.parametrize("B,T,L", [(3, 102400, 48000), (2, 102400, 30000), (2, 30000, 96000), (1, 2048, 2048),
                                    (2, 102400, 96000), (1, 131072, 120000)])
 def test_reverb_grad_oracle(dd, B, T, L):
     g = torch.Generator().manual_seed(B * T + L)

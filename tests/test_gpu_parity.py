@@ -508,7 +508,7 @@ def test_noise_params_golden(dd):
     assert rms(out, g["out"]) < 1e-7, rms(out, g["out"])
 
 
-@pytest.mark.parametrize("nb_blocks,L", [(3, 300), (50, 48000), (100, 48000), (50, 96000), (120, 250000)])
+@pytest.mark.parametrize("nb_blocks,L", [(3, 300), (50, 48000), (50, 30000), (100, 48000), (50, 96000), (120, 250000)])
 def test_reverb_partitioned_shapes(dd, nb_blocks, L):
     """UPOLS (LDS-tiled MAC and the global-memory MAC for very long IRs) vs fp64 convolution."""
     T = nb_blocks * 2048 - 17

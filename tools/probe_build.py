@@ -30,6 +30,33 @@ PROBES = {
                ("      ehp = hnew;\n    }\n", "      ehp = hnew;\n    }\n    " + _STAMP.format(k=3) + "\n"),
                ("      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n",
                 "      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n      " + _STAMP.format(k=4) + "\n")],
+    # wgclk: per-workgroup start / end realtime stamps (100 MHz) and hardware ids of the fused synthesis
+    # kernel, in a device table read back by ddsp_probe_wg_stamps (tools/exp_wg_tail.py): the grid's
+    # 3.125 rounds of resident workgroups and how busy the chip is in the last one
+    "wgclk": [("  extern __shared__ float4 smem4[];\n  __shared__ double red[32];\n  float acc[4], nz[4];\n",
+               "  extern __shared__ float4 smem4[];\n  __shared__ double red[32];\n  float acc[4], nz[4];\n"
+               "  const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime();\n"),
+              ("make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121\n}\n",
+               "make_float4(acc[0] + nz[0], acc[1] + nz[1], acc[2] + nz[2], acc[3] + nz[3]);  // decoder.py:121\n"
+               "  if (threadIdx.x == 0) {\n"
+               "    uint32_t hw, xcc;\n"
+               "    asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\" : \"=s\"(hw));\n"
+               "    asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\" : \"=s\"(xcc));\n"
+               "    const uint64_t i = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;\n"
+               "    if (i < kProbeWG) {\n"
+               "      g_probe_stamps[3 * i] = probe_t0;\n"
+               "      g_probe_stamps[3 * i + 1] = __builtin_amdgcn_s_memrealtime();\n"
+               "      g_probe_stamps[3 * i + 2] = ((uint64_t)xcc << 32) | hw;\n"
+               "    }\n"
+               "  }\n}\n"),
+              ("template <bool RNG, bool SPLIT, bool CTRL, bool PREFIX>\n__global__",
+               "constexpr uint64_t kProbeWG = 65536;\n__device__ uint64_t g_probe_stamps[3 * kProbeWG];\n"
+               "template <bool RNG, bool SPLIT, bool CTRL, bool PREFIX>\n__global__"),
+              ("int ddsp_hip_frame_phase_prefix(",
+               "int ddsp_probe_wg_stamps(uint64_t* host, int64_t n) {\n"
+               "  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe_stamps), sizeof(uint64_t) * 3 * n, 0,\n"
+               "                                  hipMemcpyDeviceToHost);\n}\n\n"
+               "int ddsp_hip_frame_phase_prefix(")],
     "gru8": [("gru_forward_launch<16, 32>", "gru_forward_launch<8, 64>"),
              ("gru_backward_steps<16, 32>", "gru_backward_steps<8, 64>")],
     "gru32": [("gru_forward_launch<16, 32>", "gru_forward_launch<32, 16>"),
