@@ -56,13 +56,27 @@ def main():
     below = grid[active < 0.9 * peak]
     tail_start = float(below[below > span * 0.3].min()) if (below > span * 0.3).any() else span
     xcc = (st[:, 2] >> np.uint64(32)).astype(np.int64)
-    out = {"span_us": round(float(span), 2), "peak_resident_wg": int(peak),
+    hw = (st[:, 2] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    cu = xcc * 256 + ((hw >> 8) & 0xFF)  # HW_ID [15:8]: cu_id, sh_id, se_id
+    per_cu_peak = []
+    for c in np.unique(cu):
+        m = cu == c
+        ev = sorted([(t, 1) for t in s[m]] + [(t, -1) for t in e[m]], key=lambda x: (x[0], x[1]))
+        cur = top = 0
+        for _, d in ev:
+            cur += d
+            top = max(top, cur)
+        per_cu_peak.append(top)
+    occ = {str(t): _lib.load().ddsp_probe_occupancy(ctypes.c_int(t), ctypes.c_int64(6480)) for t in (64, 128, 256)}
+    out = {"span_us": round(float(span), 2), "peak_resident_wg": int(peak), "runtime_occupancy_blocks_per_cu": occ,
            "fill_efficiency": round(float(dur.sum() / (span * peak)), 4),
            "tail_from_us": round(tail_start, 2),
            "wg_time_in_tail_frac": round(float(np.clip(np.minimum(e, span) - np.maximum(s, tail_start), 0,
                                                         None).sum() / dur.sum()), 4),
            "rounds": rounds,
            "wg_per_xcc": np.bincount(xcc, minlength=8).tolist(),
+           "distinct_cus": int(np.unique(cu).size),
+           "per_cu_peak_resident": {str(k): int(v) for k, v in zip(*np.unique(per_cu_peak, return_counts=True))},
            "xcc_span_us": [round(float(e[xcc == x].max() - s[xcc == x].min()), 2) for x in range(8)],
            "active_every_5us": active[::10].tolist()}
     print(json.dumps(out), flush=True)

@@ -53,10 +53,17 @@ PROBES = {
                "constexpr uint64_t kProbeWG = 65536;\n__device__ uint64_t g_probe_stamps[3 * kProbeWG];\n"
                "template <bool RNG, bool SPLIT, bool CTRL, bool PREFIX>\n__global__"),
               ("int ddsp_hip_frame_phase_prefix(",
+               "int ddsp_probe_occupancy(int threads, int64_t shm) {\n"
+               "  int n = -1;\n"
+               "  hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, synth_frame_kernel<true, false, false, false>, threads,\n"
+               "                                               (size_t)shm);\n"
+               "  return n;\n}\n\n"
                "int ddsp_probe_wg_stamps(uint64_t* host, int64_t n) {\n"
                "  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe_stamps), sizeof(uint64_t) * 3 * n, 0,\n"
                "                                  hipMemcpyDeviceToHost);\n}\n\n"
                "int ddsp_hip_frame_phase_prefix(")],
+    # wgclk with the kernel's SGPRs capped at 80 (does the 14-workgroups-per-CU residency move?)
+    "wgclksg": None,
     "gru8": [("gru_forward_launch<16, 32>", "gru_forward_launch<8, 64>"),
              ("gru_backward_steps<16, 32>", "gru_backward_steps<8, 64>")],
     "gru32": [("gru_forward_launch<16, 32>", "gru_forward_launch<32, 16>"),
@@ -75,6 +82,11 @@ PROBES = {
     "noosc": [("osc_bank4(coef, H4, w, acc);", "acc[0] = w[0]; acc[1] = w[1]; acc[2] = w[2]; acc[3] = w[3];")],
     "nofir": [("float4 y = fir4(h, x, j0, lo_end, bs, bs);", "float4 y = make_float4(x[j0], x[j0 + 1], h[j0], h[j0 + 3]);")],
 }
+
+
+PROBES["wgclksg"] = PROBES["wgclk"] + [
+    ("__global__ void __launch_bounds__(256) synth_frame_kernel(",
+     "__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) synth_frame_kernel(")]
 
 
 def build(name):
