@@ -348,8 +348,56 @@ __global__ void __launch_bounds__(kNT) upols_mac_ring_kernel(const float2* __res
     if (b0 + d >= 0) Yp[(int64_t)(b0 + d) * kN] = make_float2(acc[d].x, acc[d].y);
 }
 
-// The adjoint MAC's whole-row form (upols_mac_adj_stream_kernel) for the row length it is built for:
-// 50 blocks (config 2's 102400 samples), up to 25 kernel windows (a 1 s IR at 48 kHz)
+
+// The same sums for a whole pair row in one thread (nb == NBK, Q <= NQ): every Z_m and G_q of the bin is
+// loaded once and stays in registers (the ring kernel's two 25-block chunks re-read ~1.5x of Z: 122 vs
+// 104 MB at config 2), and the outputs stream — step b issues the loads of step b + PF (Z_{b+PF},
+// G_{b+PF}), then forms Y_b = sum_{q <= min(b, NQ-1)} Z_{b-q} G_q from operands already in registers and
+// stores it, so loads, products and stores overlap inside every wave (166 VGPRs; grid N/256 x npairs:
+// one round at 2 waves per SIMD).  Same-box A/Bs at config 2 (profiles/r05_ab_mac_vjp.log): 24.5-24.8 us
+// against 32.1-32.4 us for the ring kernel on boxes where the ring runs 32 us (step -3.8 / -6.4 us), equal
+// (25.0 vs 24.9-25.0 us) where the ring runs 25 us.  The ring kernel serves the other shapes.
+template <int NBK, int NQ, int PF>
+__global__ void __launch_bounds__(kNT) upols_mac_stream_kernel(const float2* __restrict__ X,
+                                                               const float2* __restrict__ Hs,
+                                                               int64_t h_pair_stride, int nb, int Q,
+                                                               float2* __restrict__ Y) {
+  constexpr int kRow = kN * (int)sizeof(float2);
+  const int f = blockIdx.x * kNT + threadIdx.x;
+  const int pair = blockIdx.y;
+  const float2* Xrow = X + (int64_t)pair * nb * kN;
+  const float2* Hrow = Hs + (int64_t)pair * h_pair_stride;
+  const int voff = f * (int)sizeof(float2);
+  float2 z[NBK], g[NQ];
+  auto zload = [&](int m) { z[m] = row_load<DDSP_MAC_ZAUX>(Xrow + (int64_t)m * kN, kRow, voff); };
+  auto gload = [&](int q) { g[q] = row_load<DDSP_MAC_GAUX>(Hrow + (int64_t)min(q, Q - 1) * kN, q < Q ? kRow : 0, voff); };
+#pragma unroll
+  for (int s = 0; s < PF; ++s) {
+    if (s < NQ) gload(s);
+    zload(s);
+  }
+  float2* Yp = Y + (int64_t)pair * nb * kN + f;
+#pragma unroll
+  for (int b = 0; b < NBK; ++b) {
+    if (b + PF < NQ) gload(b + PF);
+    if (b + PF < NBK) zload(b + PF);
+    __builtin_amdgcn_sched_barrier(0);
+    v2f acc = {0.f, 0.f}, acc2 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q <= b) {
+        const float2 h = g[q];
+        if (q & 1) cmac(acc2, z[b - q], (v2f){h.x, h.y}, (v2f){-h.y, h.x});
+        else cmac(acc, z[b - q], (v2f){h.x, h.y}, (v2f){-h.y, h.x});
+      }
+    }
+    Yp[(int64_t)b * kN] = make_float2(acc.x + acc2.x, acc.y + acc2.y);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The whole-row MAC forms (upols_mac_stream_kernel, upols_mac_adj_stream_kernel) for the row length they
+// are built for: 50 blocks (config 2's 102400 samples), up to 25 kernel windows (a 1 s IR at 48 kHz)
 constexpr int kStreamNB = 50, kStreamNQ = 25, kStreamPF = 4;
 
 // y[row][bP + n] = IFFT(Y_b)[P + n]; grid (nb, npairs)
@@ -506,8 +554,6 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_ring_kernel(const float2* _
 // k = NBK-1-s, from GZ_k..GZ_{k+s} and H_0..H_s already in registers and stores it, so loads, products
 // and stores overlap inside every wave (166 VGPRs; grid N/256 x npairs, one round at 2 waves/SIMD).
 // Config 2: 23.1-23.2 us against 29.8-29.9 for the ring kernel (same box, tools/ab_prof.sh reverb_bwd).
-// The same form of the forward MAC measured no faster than its ring kernel there (25.0 vs 24.9-25.0 us:
-// the forward ring's non-temporal loads already stream at ~4.9 TB/s), so the forward keeps the ring.
 template <int NBK, int NQ, int PF>
 __global__ void __launch_bounds__(kNT) upols_mac_adj_stream_kernel(const float2* __restrict__ G,
                                                                    const float2* __restrict__ Hs, int nb, int Q,
@@ -654,6 +700,11 @@ int upols_apply_spectra(const float2* Z, int64_t rows, int64_t n, const float* s
   // an LDS-tiled variant that reads Z once, 25%: lower occupancy, exposed loads; every operand
   // loaded up front from registers, 40%: 202 VGPRs, 2 waves/SIMD; one thread per (pair, bin)
   // streaming all blocks with a register ring, 8%)
+  if (nb == kStreamNB && Q <= kStreamNQ)
+    hipLaunchKernelGGL((upols_mac_stream_kernel<kStreamNB, kStreamNQ, kStreamPF>), dim3(kN / kNT, (unsigned)npairs),
+                       dim3(kNT), 0, S(stream), Z, reinterpret_cast<const float2*>(spectrum), h_stride, (int)nb,
+                       (int)Q, Y);
+  else
   hipLaunchKernelGGL((upols_mac_ring_kernel<RB, kRingPF, kRingGR>),
                      dim3(kN / kNT, (unsigned)((nb + RB - 1) / RB), (unsigned)npairs), dim3(kNT), 0, S(stream), Z,
                      reinterpret_cast<const float2*>(spectrum), h_stride, (int)nb, (int)Q, Y);

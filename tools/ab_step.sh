@@ -22,7 +22,7 @@ ks = {}
 for f in glob.glob(d + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        for short, key in (("synth", "synth_frame_kernel"), ("mac", "upols_mac_ring"), ("fwd", "upols_forward"), ("inv", "upols_inverse")):
+        for short, key in (("synth", "synth_frame_kernel"), ("mac", "upols_mac_"), ("fwd", "upols_forward"), ("inv", "upols_inverse")):
             if key in n:
                 ks[short] = float(r["AverageNs"]) / 1e3
 print(f"{v:10s} step {b['ms_per_step']:.4f} ms  synth(in-region) {b['roofline']['avg_launch_ms']:.4f}  rocprof " +

@@ -25,13 +25,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # inverse reads the Y spectra exactly once (51.2 MB at config 2) and reports 25.7 MB; the forward
 # reads the signal exactly once (26.2 MB) and reports 12.9 MB
 WIDE_READS = ("harmonic_samples_tiled_kernel", "upols_forward_kernel", "upols_forward_ir_kernel", "upols_inverse_kernel",
-              "upols_mac_kernel", "upols_mac_ring_kernel")
+              "upols_mac_kernel", "upols_mac_ring_kernel", "upols_mac_stream_kernel")
 REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch of it
     "synth_frame_kernel": ("synth_frame_kernel",),
     "harmonic_frames_kernel": ("harmonic_frames_kernel",),
     "harmonic_samples_kernel": ("phase_chunk_sums_kernel", "harmonic_samples_tiled_kernel"),
     "filtered_noise_kernel": ("filtered_noise_kernel",),
-    "reverb": ("upols_forward_kernel", "upols_forward_ir_kernel", "upols_mac_kernel", "upols_mac_ring_kernel", "upols_inverse_kernel"),
+    "reverb": ("upols_forward_kernel", "upols_forward_ir_kernel", "upols_mac_kernel", "upols_mac_ring_kernel",
+               "upols_mac_stream_kernel", "upols_inverse_kernel"),
 }
 
 
