@@ -227,13 +227,25 @@ __device__ __forceinline__ float dpp_sum8(float v) {
   return v;
 }
 
+// An aborted launch (a workgroup that could not be resident within kPSpinTicks, e.g. beside another
+// long-running kernel) must not leave plausible values behind: every workgroup that sees the abort fills
+// the outputs with NaN (grid-strided), so the failure propagates visibly instead of as garbage.
+__device__ void gru_persistent_poison(float* __restrict__ out, float* __restrict__ h_last, int B, int T) {
+  const float qnan = __int_as_float(0x7fc00000);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < (int64_t)B * T * kPH; i += stride) out[i] = qnan;
+  if (h_last)
+    for (int64_t i = i0; i < (int64_t)B * kPH; i += stride) h_last[i] = qnan;
+}
+
 template <bool kLocal>
 __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp, const float* __restrict__ w_hh,
                                                     const float* __restrict__ b_hh, const float* __restrict__ h0,
                                                     float* __restrict__ h_last, float* __restrict__ save, int B, int T,
                                                     int g, int s, uint32_t* __restrict__ counter,
                                                     uint32_t* __restrict__ abort_word, __amdgpu_buffer_rsrc_t rout,
-                                                    float* hs, float (*part)[kPR][kPI], int* s_abort) {
+                                                    float* hs, float (*part)[kPR][kPI], int* s_abort,
+                                                    float* __restrict__ out) {
   constexpr int kStoreAux = kLocal ? 0 : 16;  // write-back into the XCD's L2, or write-through (sc1)
   const int nI = B > g ? (B - g + kPG - 1) / kPG : 0;  // items of this group
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -280,7 +292,10 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
     if (t > 0) {  // every slot of the group has published h_{t-1}
       if (tid == 0 && !wait_at_least(counter, (uint32_t)kPS * (uint32_t)t, abort_word)) *s_abort = 1;
       __syncthreads();
-      if (*s_abort) return;
+      if (*s_abort) {
+        gru_persistent_poison(out, h_last, B, T);
+        return;
+      }
     }
     // h_{t-1} of the group's items into LDS, once per step (zeros past nI)
     {
@@ -398,7 +413,10 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
     s_slot = local ? (int)ticket : (int)(blockIdx.x / kPG);
   }
   __syncthreads();
-  if (s_abort) return;
+  if (s_abort) {
+    gru_persistent_poison(out, h_last, B, T);
+    return;
+  }
   const int g = s_group, s = s_slot;
   if (B <= g) return;  // the group has no items: nobody waits for it
   // out as a buffer resource: byte offsets (< 2^31, checked by the host) with cache-policy bits
@@ -406,10 +424,10 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
   uint32_t* counter = sync + g * kPCounterStride;
   if (s_local)
     gru_persistent_body<true>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
-                              &s_abort);
+                              &s_abort, out);
   else
     gru_persistent_body<false>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
-                               &s_abort);
+                               &s_abort, out);
 }
 
 // ---------------------------------------------------------------------------------------
