@@ -298,7 +298,8 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
  * items g, g + 8, ...; each workgroup keeps its 48 rows of W_hh in LDS for the whole sequence and the
  * group's slots hand h_t to each other through the output sequence (write-through stores, a per-group
  * counter).  Needs all 256 workgroups resident together (one per CU): launched on a stream whose kernels
- * cannot reach every CU, it ends after a bounded wait with garbage output rather than hang.  Workspace:
+ * cannot reach every CU, it ends after a bounded wait (200 ms) with out and h_last filled with NaN rather
+ * than hang or leave plausible values.  Workspace:
  * ddsp_hip_gru_persistent_workspace_size() bytes (zeroed by the call, on the stream, by a kernel of its own:
  * the call stays capturable into a HIP graph). */
 size_t ddsp_hip_gru_persistent_workspace_size(void);
