@@ -144,7 +144,9 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
   const int n = NOISE ? 2 * (NB - 1) : 0, half = n >> 1;
   const int qmax = min(n, bs);
   const bool quads = NOISE && (half % 4 == 0) && n <= bs && (bs % 4 == 0);
-  const int npart_len = NSEG * (quads ? n : qmax);
+  // quads: segment rows n + 4 floats apart, so the rows of one wave's segments start on different banks
+  // (48.1-48.2 -> 47.2-47.5 us for the noise VJP at config 2, same box)
+  const int npart_len = NSEG * (quads ? n + 4 : qmax);
   float* xl = smem + ((hfl + 3) & ~3);                              // [bs] noise
   float* ct = xl + bs;                                               // [n] cos(2 pi q / n)
   float* e = ct + n;                                                 // [n] windowed tap gradients
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
             acc.w = fmaf(gl[j0 + d + 3], xv, acc.w);
           }
         }
-        float* dst = npart + seg * n + q0;
+        float* dst = npart + seg * (n + 4) + q0;
         dst[0] = acc.x;
         dst[1] = acc.y;
         dst[2] = acc.z;
@@ -379,7 +381,7 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
       if (q < qmax) {
         if (quads) {
           const int ns_q = q >= half ? NSEG : 1;
-          for (int s = 0; s < ns_q; ++s) v += npart[s * n + q];
+          for (int s = 0; s < ns_q; ++s) v += npart[s * (n + 4) + q];
         } else {
           for (int s = 0; s < NSEG; ++s) v += npart[s * qmax + q];
         }
@@ -468,7 +470,7 @@ size_t frame_backward_lds_floats(bool harm, bool noise, int H, int bs, int NS, i
   const int n = 2 * (NB - 1);
   const int qmax = std::min(n, bs);
   const bool quads = ((n / 2) % 4 == 0) && n <= bs && bs % 4 == 0;
-  const size_t npart_len = (size_t)NSEG * (quads ? n : qmax);
+  const size_t npart_len = (size_t)NSEG * (quads ? n + 4 : qmax);
   const size_t off_xl = (hfl + 3) & ~(size_t)3;
   const size_t off_gl = (off_xl + (size_t)bs + 2 * (size_t)n + npart_len + 3) & ~(size_t)3;
   return off_gl + (size_t)bs + 8;
