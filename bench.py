@@ -236,10 +236,12 @@ def cpu_baseline(args, rank_inputs_seed=0):
                       f"{sweep_b} items; host os.cpu_count() = {host})"}
 
 
-def train_leg(args, inp, dev, reps=20):
+def train_leg(args, inp, dev, reps=100):
     """one training step of the synthesis path — forward (synth_frames +
     reverb) and backward (reverb input/IR gradients, harmonic and noise VJPs) for an upstream
-    gradient w, i.e. what train.py:84-130 runs below the decoder network."""
+    gradient w, i.e. what train.py:84-130 runs below the decoder network.  Timed at steady state, as a
+    training loop runs it: 10 untimed steps, then `reps` (0.05 s of steps at config 2; 20 steps after 3
+    read 2-5 % high, as the first steps of a loop do)."""
     from ddsp_pytorch_amd import core
     from ddsp_pytorch_amd.modules import Reverb
     B, F, H, NB, bs, sr = (args.batch, args.frames, args.harmonics, args.bands, args.block_size,
@@ -266,7 +268,7 @@ def train_leg(args, inp, dev, reps=20):
             ev["forward"].append((e[0], e[1]))
             ev["backward"].append((e[1], e[2]))
 
-    for _ in range(3):
+    for _ in range(10):
         step(False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
