@@ -240,8 +240,8 @@ def train_leg(args, inp, dev, reps=100):
     """one training step of the synthesis path — forward (synth_frames +
     reverb) and backward (reverb input/IR gradients, harmonic and noise VJPs) for an upstream
     gradient w, i.e. what train.py:84-130 runs below the decoder network.  Timed at steady state, as a
-    training loop runs it: 10 untimed steps, then `reps` (0.05 s of steps at config 2; 20 steps after 3
-    read 2-5 % high, as the first steps of a loop do)."""
+    training loop runs it: 10 untimed steps, then `reps` (0.05 s of steps at config 2; 20 steps read about
+    1 % higher on one box: 0.5289-0.5340 vs 0.5234-0.5277 ms)."""
     from ddsp_pytorch_amd import core
     from ddsp_pytorch_amd.modules import Reverb
     B, F, H, NB, bs, sr = (args.batch, args.frames, args.harmonics, args.bands, args.block_size,
