@@ -420,8 +420,10 @@ __global__ void __launch_bounds__(kNT) upols_inverse_kernel(const float2* __rest
     const int64_t s = (int64_t)b * kP + j + 256 * r - kP;
     if (s < T) {
       const int64_t so = reverse ? T - 1 - s : s;
-      ya[so] = v[r].x;
-      if (yb) yb[so] = v[r].y;
+      // non-temporal: the reverb's output is not read again by the step (16.6 vs 17.6 us at config 2,
+      // the next synthesis launch unchanged, same-box A/B)
+      __builtin_nontemporal_store(v[r].x, ya + so);
+      if (yb) __builtin_nontemporal_store(v[r].y, yb + so);
     }
   }
 }
