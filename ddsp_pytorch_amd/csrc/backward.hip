@@ -462,6 +462,193 @@ __global__ void __launch_bounds__(512) frame_backward_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The noise VJP alone (FilteredNoise's backward, modules.py:116-128) at the reference's 65 bands
+// (n = 128 filter taps) and bs % 128 == 0, bs >= 512: one WAVE per frame, no workgroup barrier after the
+// cosine table.
+//   dh[j] = sum_d g[j + d] x[d] for the taps the filter has: j in [0, 64) (lags < bs - j) and
+//   j in [bs - 64, bs) (lags < bs - j <= 64).  g is zero-padded past bs, so every lane runs a fixed
+//   rectangle: the long taps as 8 tap groups x 8 lag segments of L = bs/8 lags (8 taps x 4 lags per
+//   ds_read_b128 of g and one of x: 32 FMAs per two reads), the short taps as 8 tap groups x 8 segments
+//   of 8 lags.
+//   Bank-conflict-free LDS reads: ds_read_b128 serves a wave in four 16-lane groups (MI355X_MICROARCH.md
+//   §LDS); each group holds the 8 tap groups of two lag segments (kNvjpLane), and every segment reads its
+//   own copy of its g window [sL, sL + L + 72) and its own x run, at strides of L + 76 and L + 4 floats
+//   (= 4 mod 8): the two segments of a group fall on disjoint bank halves.  (A first form with one shared
+//   g array and x at 64-float segment strides ran 51 us at config 2: 4- and 8-way conflicts.)
+//   e[q] = dh[j(q)] hann[q] (q >= 64: j = q - 64; q < 64: j = q - 64 + bs), then
+//   dA_k = (c_k / n)(-1)^k [e_0 + (-1)^k e_64 + sum_{q=1}^{63} s_q cos(2 pi q k / n)] for k < 64 with the
+//   folded sums s_q = e_q + e_{n-q}, and the Nyquist band k = 64 from the alternating sum (as
+//   frame_backward_kernel).
+constexpr int kNvjpWaves = 4;  // frames per workgroup
+__host__ __device__ constexpr int nvjp_gstride(int L) { return L + 76; }
+__host__ __device__ constexpr int nvjp_xstride(int L) { return L + 4; }
+__host__ __device__ constexpr int nvjp_wave_floats(int bs) {
+  return 8 * nvjp_gstride(bs / 8) + 8 * nvjp_xstride(bs / 8) + 192;
+}
+// lane -> 16 * (lag segment pair) + 8 * (segment in the pair) + tap group, so that the lanes of each
+// ds_read_b128 group {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} (+32) are the 16 (segment, tap group) of one
+// segment pair
+__device__ constexpr unsigned char kNvjpLane[64] = {
+    0,  1,  2,  3,  16, 17, 18, 19, 20, 21, 22, 23, 4,  5,  6,  7,  24, 25, 26, 27, 8,  9,  10, 11,
+    12, 13, 14, 15, 28, 29, 30, 31, 32, 33, 34, 35, 48, 49, 50, 51, 52, 53, 54, 55, 36, 37, 38, 39,
+    56, 57, 58, 59, 40, 41, 42, 43, 44, 45, 46, 47, 60, 61, 62, 63};
+
+// acc[i] += sum_{d < 16 NQ4} g[i + d] x[d], i < 8, with g4 / x4 at the lane's window: per 4 lags one
+// ds_read_b128 of x and one of g (a 4-quad register ring, indexed statically in the unrolled body)
+template <int NQ4>
+__device__ __forceinline__ void corr8(const float4* __restrict__ g4, const float4* __restrict__ x4, float (&acc)[8]) {
+  float4 w[4];
+  w[0] = g4[0];
+  w[1] = g4[1];
+  w[2] = g4[2];
+#pragma unroll  // fully: a loop-carried ring was scalarised into ds_read2_b32 pairs
+  for (int c = 0; c < NQ4; ++c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 xv = x4[4 * c + k];
+      w[(k + 3) & 3] = g4[4 * c + k + 3];
+      const float4 a = w[k & 3], b = w[(k + 1) & 3], e = w[(k + 2) & 3];
+      const float win[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e.x, e.y, e.z, e.w};
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = fmaf(win[i + l], xs[l], acc[i]);
+      }
+    }
+  }
+}
+
+template <int NOISE, bool RAW>
+__global__ void __launch_bounds__(64 * kNvjpWaves) noise_vjp_wave_kernel(
+    const float* __restrict__ grad, const float* __restrict__ mags, const float* __restrict__ noise, uint32_t k0,
+    uint32_t k1, uint32_t off0, uint32_t off1, float bias, float* __restrict__ d_mags, int64_t frames, int bs) {
+  constexpr int n = 128, half = 64, NB = 65;
+  extern __shared__ float4 smem_nv[];
+  float* ct = reinterpret_cast<float*>(smem_nv);  // [n]
+  fill_cos_table(ct, n);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t frame = (int64_t)blockIdx.x * kNvjpWaves + wave;
+  if (frame >= frames) return;
+  const int L = bs >> 3, Sg = nvjp_gstride(L), Sx = nvjp_xstride(L);
+  float* gc = ct + n + wave * nvjp_wave_floats(bs);  // [8][Sg] window copies of g (zero past bs)
+  float* xc = gc + 8 * Sg;                           // [8][Sx] the noise, one run per lag segment
+  float* es = xc + 8 * Sx;                           // [128] e, then [64] s
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  // ---- loads: the 8 windows of g (the upstream gradient of the frame) and the frame's noise ----
+  const float* gf = grad + frame * bs;
+  const int wq = (L + 72) >> 2;  // quads per window
+  for (int i = lane; i < 8 * wq; i += 64) {
+    const int s = i / wq, u = s * L + 4 * (i - s * wq);
+    const float4 v = u < bs ? *reinterpret_cast<const float4*>(gf + u) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(gc + s * Sg + (u - s * L)) = v;
+  }
+  const int quads = bs >> 2;
+  for (int t = lane; t < quads; t += 64) {
+    float4 v;
+    if (NOISE == 2) {  // the forward's Philox stream (synth_frame.hip / noise.hip counter layout)
+      const uint64_t qc = (uint64_t)frame * (uint64_t)quads + (uint64_t)t;
+      const Philox4 r = philox4x32_10((uint32_t)qc, (uint32_t)(qc >> 32), off0, off1, k0, k1);
+      v = make_float4(uniform_pm1(r.v[0]), uniform_pm1(r.v[1]), uniform_pm1(r.v[2]), uniform_pm1(r.v[3]));
+    } else {
+      v = *reinterpret_cast<const float4*>(noise + frame * bs + 4 * t);
+    }
+    const int s = (4 * t) / L;
+    *reinterpret_cast<float4*>(xc + s * Sx + (4 * t - s * L)) = v;
+  }
+  wsync();
+
+  // ---- correlation ----
+  const int m = kNvjpLane[lane];
+  const int tg = m & 7, seg = m >> 3;
+  float accL[8], accS[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) accL[i] = accS[i] = 0.0f;
+  {
+    // long taps j = 8 tg + i, lags [seg L, seg L + L): window copy seg at offset 8 tg
+    const float4* g4 = reinterpret_cast<const float4*>(gc + seg * Sg + 8 * tg);
+    const float4* x4 = reinterpret_cast<const float4*>(xc + seg * Sx);
+    int c = 0;
+    for (; c + 64 <= L; c += 64) corr8<4>(g4 + c / 4, x4 + c / 4, accL);  // (L = 64 at bs = 512: one call)
+    if (L & 32) {
+      corr8<2>(g4 + c / 4, x4 + c / 4, accL);
+      c += 32;
+    }
+    if (L & 16) corr8<1>(g4 + c / 4, x4 + c / 4, accL);
+  }
+  {
+    // short taps j = bs - 64 + 8 tg + i, lags [8 seg, 8 seg + 8): in window copy 7 (which starts at bs - L)
+    const float4* g4 = reinterpret_cast<const float4*>(gc + 7 * Sg + (L - 64) + 8 * tg + 8 * seg);
+    const float4* x4 = reinterpret_cast<const float4*>(xc + 8 * seg);
+    const float4 w0 = g4[0], w1 = g4[1], w2 = g4[2], w3 = g4[3];
+    const float4 x0 = x4[0], x1 = x4[1];
+    const float win[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+    const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) accS[i] = fmaf(win[i + l], xs[l], accS[i]);
+    }
+  }
+  wsync();  // every lane's g / x reads are done: the partials overwrite the g windows
+  float* partL = gc;        // [8 seg][64 taps]
+  float* partS = gc + 512;  // [8 seg][64 taps]
+  *reinterpret_cast<float4*>(partL + seg * 64 + 8 * tg) = make_float4(accL[0], accL[1], accL[2], accL[3]);
+  *reinterpret_cast<float4*>(partL + seg * 64 + 8 * tg + 4) = make_float4(accL[4], accL[5], accL[6], accL[7]);
+  *reinterpret_cast<float4*>(partS + seg * 64 + 8 * tg) = make_float4(accS[0], accS[1], accS[2], accS[3]);
+  *reinterpret_cast<float4*>(partS + seg * 64 + 8 * tg + 4) = make_float4(accS[4], accS[5], accS[6], accS[7]);
+  wsync();
+
+  // ---- e[q] (lane l: q = l, the short tap l; q = 64 + l, the long tap l) and the alternating sum ----
+  float eS = 0.0f, eL = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    eS += partS[s * 64 + lane];
+    eL += partL[s * 64 + lane];
+  }
+  eS *= 0.5f - 0.5f * ct[lane];
+  eL *= 0.5f - 0.5f * ct[half + lane];
+  es[lane] = eS;
+  es[half + lane] = eL;
+  double alt = (lane & 1) ? -(double)eS - (double)eL : (double)eS + (double)eL;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
+  wsync();
+  float* sq = es + n;  // [64] s_q = e_q + e_{n-q} (q >= 1)
+  sq[lane] = lane ? eS + es[n - lane] : 0.0f;
+  wsync();
+
+  // ---- cosine transform: lane k < 64 ----
+  const int k = lane;
+  float v0 = 0.0f, v1 = 0.0f;
+#pragma unroll
+  for (int q4 = 0; q4 < 16; ++q4) {
+    const float4 s4 = *reinterpret_cast<const float4*>(sq + 4 * q4);
+    const float c0 = ct[(k * (4 * q4)) & (n - 1)], c1 = ct[(k * (4 * q4 + 1)) & (n - 1)];
+    const float c2 = ct[(k * (4 * q4 + 2)) & (n - 1)], c3 = ct[(k * (4 * q4 + 3)) & (n - 1)];
+    v0 = fmaf(s4.x, c0, v0);  // (s_0 = 0)
+    v1 = fmaf(s4.y, c1, v1);
+    v0 = fmaf(s4.z, c2, v0);
+    v1 = fmaf(s4.w, c3, v1);
+  }
+  const float inv_n = 1.0f / (float)n;
+  float dA = (v0 + v1 + es[0] + ((k & 1) ? -es[half] : es[half])) * (k == 0 ? 1.0f : 2.0f) * inv_n;
+  if (k & 1) dA = -dA;
+  float* dm = d_mags + frame * NB;
+  const float* mg = RAW ? mags + frame * NB : nullptr;
+  dm[k] = RAW ? dA * scale_fn_grad(mg[k] + bias) : dA;
+  if (lane == 0) {
+    const float dN = (float)alt * inv_n;  // k = half (even)
+    dm[half] = RAW ? dN * scale_fn_grad(mg[half] + bias) : dN;
+  }
+}
+
 // LDS floats of frame_backward_kernel (its layout, written out on the host)
 size_t frame_backward_lds_floats(bool harm, bool noise, int H, int bs, int NS, int NB, int NSEG) {
   const size_t SL = (size_t)(((bs + NS - 1) / NS + 1) & ~1);
@@ -624,6 +811,25 @@ static int frame_backward_launch(int hmode, int noise_mode, bool raw, const floa
   if (noise_mode && NB < 2) return DDSP_HIP_EINVAL;
   if (batch == 0 || frames == 0) return DDSP_HIP_OK;
   if (batch > 65535 || frames > INT32_MAX || H > 4096 || bs > 8192 || NB > 4097) return DDSP_HIP_ERANGE;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
+  // noise alone at the reference's 65 bands: one wave per frame (noise_vjp_wave_kernel)
+  if (hmode == 0 && NB == 65 && bs % 128 == 0 && bs >= 512 && bs <= 1024 && ((uintptr_t)grad & 15) == 0 &&
+      (noise_mode == 2 || ((uintptr_t)noise & 15) == 0)) {
+    const int64_t rows = batch * frames;
+    const dim3 grid((unsigned)((rows + kNvjpWaves - 1) / kNvjpWaves));
+    const size_t shm = sizeof(float) * (128 + (size_t)kNvjpWaves * nvjp_wave_floats((int)bs));  // 29.7 KB at bs 512
+#define DDSP_NVJP_LAUNCH(N_, R_)                                                                                \
+  hipLaunchKernelGGL((noise_vjp_wave_kernel<N_, R_>), grid, dim3(64 * kNvjpWaves), shm, S(stream), grad, mags, \
+                     noise, k0, k1, o0, o1, bias, d_mags, rows, (int)bs)
+    if (noise_mode == 1) {
+      if (raw) DDSP_NVJP_LAUNCH(1, true); else DDSP_NVJP_LAUNCH(1, false);
+    } else {
+      if (raw) DDSP_NVJP_LAUNCH(2, true); else DDSP_NVJP_LAUNCH(2, false);
+    }
+#undef DDSP_NVJP_LAUNCH
+    return launch_status();
+  }
   // noise alone: 128 threads per frame (config 2: 53.8 us; 64 threads 60.5, 256 threads 70.0)
   int nt = 128, ns = 1;
   if (hmode) harmonic_backward_shape((int)H, (int)bs, nt, ns);
@@ -635,8 +841,6 @@ static int frame_backward_launch(int hmode, int noise_mode, bool raw, const floa
                                                                (int)NB, nseg);
   if (shm > 150 * 1024) return DDSP_HIP_ERANGE;
   const dim3 grid((unsigned)frames, (unsigned)batch);
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const uint32_t o0 = (uint32_t)offset, o1 = (uint32_t)(offset >> 32);
 #define DDSP_FB_LAUNCH(HM_, N_, R_)                                                                         \
   hipLaunchKernelGGL((frame_backward_kernel<HM_, N_, R_>), grid, dim3(nt), shm, S(stream), f0, grad, param, amp, \
                      dist, d_param, d_amp, d_dist, (int)frames, (int)H, (int)bs, sr, ns, mags, noise, k0, k1,  \
