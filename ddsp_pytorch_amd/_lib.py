@@ -106,6 +106,8 @@ SIGNATURES = {
     "ddsp_hip_reverb_input_spectra_bytes": (_SZ, [_I64, _I64]),
     "ddsp_hip_reverb_backward_workspace_size": (_SZ, [_I64, _I64, _I64, _I]),
     "ddsp_hip_reverb_backward": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
+    "ddsp_hip_reverb_backward_params": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I64, _I64, _I64, _P,
+                                            _SZ, _P]),
     "ddsp_hip_reverb_impulse_backward_workspace_size": (_SZ, [_I64]),
     "ddsp_hip_reverb_impulse_backward": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _P, _P, _P, _P, _SZ, _P]),
 }

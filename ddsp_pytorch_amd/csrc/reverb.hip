@@ -213,6 +213,26 @@ int ddsp_hip_reverb_backward(const float* x, const float* input_spectra, const f
                         workspace, workspace_bytes, stream);
 }
 
+int ddsp_hip_reverb_backward_params(const float* x, const float* input_spectra, const float* spectrum, const float* grad,
+                                    const float* noise, const float* decay, const float* wet, float sample_rate,
+                                    float* grad_x, float* grad_noise, float* grad_decay, float* grad_wet, int64_t batch,
+                                    int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
+  if (batch < 0 || n_samples < 1 || ir_length < 1 || !noise || !decay || !wet || !grad_noise || !grad_decay ||
+      !grad_wet || !(sample_rate > 0))
+    return DDSP_HIP_EINVAL;
+  if (batch == 0) {  // no signal: no gradient reaches the impulse
+    hipError_t e = hipMemsetAsync(grad_noise, 0, sizeof(float) * ir_length, S(stream));
+    if (e == hipSuccess) e = hipMemsetAsync(grad_decay, 0, sizeof(float), S(stream));
+    if (e == hipSuccess) e = hipMemsetAsync(grad_wet, 0, sizeof(float), S(stream));
+    return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;
+  }
+  if (!grad || !spectrum || (!x && !input_spectra)) return DDSP_HIP_EINVAL;
+  const ImpulseGrad ig{noise, decay, wet, ir_length, sample_rate, grad_noise, grad_decay, grad_wet};
+  return upols_backward(x, input_spectra, spectrum, grad, batch, n_samples, ir_length, grad_x, nullptr, workspace,
+                        workspace_bytes, stream, &ig);
+}
+
 size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length) {
   (void)length;
   return 2 * sizeof(double) * kImpBlocks;

@@ -42,7 +42,20 @@ size_t upols_spectra_bytes(int64_t rows, int64_t n);
 // Backward of upols_apply with a kernel shared by all rows (pairing): dx[rows, n] (nullable) and
 // dimp[tau] = sum_rows sum_t g[row][t+tau] x[row][t] for tau < min(klen, n) (nullable).  x_spectra:
 // the forward's X (nullable: recomputed from x when dimp is requested).
+// ig (nullable): also Reverb.build_impulse's backward (modules.py:21-26) from dimp in the same launches —
+// d_noise[L] (zero at taps >= min(klen, n)) and the device scalars d_decay, d_wet; dimp may then be null.
+struct ImpulseGrad {
+  const float* noise;
+  const float* decay;
+  const float* wet;
+  int64_t L;
+  float sr;
+  float* d_noise;
+  float* d_decay;
+  float* d_wet;
+};
 size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x);
 int upols_backward(const float* x, const float* x_spectra, const float* spectrum, const float* g, int64_t rows,
-                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream);
+                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream,
+                   const ImpulseGrad* ig = nullptr);
 }  // namespace ddsp

@@ -602,8 +602,9 @@ __global__ void __launch_bounds__(kNT) upols_mac_adj_stream_kernel(const float2*
 // spectrum (with the sum inside the 24 one-lag workgroups, each read 8 groups' spectra alone:
 // 14.5 us, per-CU bandwidth)
 __global__ void __launch_bounds__(kNT) upols_corr_sum_kernel(const float2* __restrict__ part, int groups, int QG,
-                                                             float2* __restrict__ sum) {
+                                                             float2* __restrict__ sum, unsigned* __restrict__ arrivals) {
   const int f = blockIdx.x * kNT + threadIdx.x, p = blockIdx.y;
+  if (arrivals && f == 0 && p == 0) *arrivals = 0u;  // upols_corr_finish_impulse_kernel's counter
   const bool next = p + 1 < QG;
   const float sg = (f & 1) ? -1.0f : 1.0f;
   float2 v = make_float2(0.f, 0.f);
@@ -633,6 +634,81 @@ __global__ void __launch_bounds__(kNT) upols_corr_finish_kernel(const float2* __
     const int64_t s = (int64_t)p * kP + j + 256 * r - kP;
     if (s < klen) dimp[s] = v[r].x * inv_n;
   }
+}
+
+// upols_corr_finish_kernel fused with Reverb.build_impulse's backward (modules.py:21-26; reverb.hip
+// impulse_backward_kernel, the same per-tap arithmetic, so d_noise is bit-identical): workgroup p turns its
+// 2048 taps of dimp straight into d_noise and fp64 partial sums of sum dimp*noise*env and sum
+// dimp*noise*env*t; the last workgroup to arrive (counter zeroed by upols_corr_sum_kernel) reduces the
+// partials in index order (deterministic) into d_wet and d_decay and leaves the counter at 0.  Two launches
+// fewer in the train step than dimp -> impulse_backward_kernel -> impulse_backward_finish_kernel.
+__global__ void __launch_bounds__(kNT) upols_corr_finish_impulse_kernel(
+    const float2* __restrict__ sum, int64_t kc, ImpulseGrad ig, double* __restrict__ partials,
+    unsigned* __restrict__ arrivals, float* __restrict__ dimp) {
+  __shared__ float2 lds[kPad];
+  __shared__ double red[32];
+  __shared__ bool last;
+  const int p = blockIdx.x, j = threadIdx.x, Qp = gridDim.x;
+  const float2* in = sum + (int64_t)p * kN;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = in[j + 256 * r];
+  // the taps' envelope and noise ahead of the transform (independent of dimp; their latency hides under it)
+  const float d = -ig.decay[0];
+  const float sp = d > 20.0f ? d : log1pf(expf(d));
+  const float neg = -sp;
+  const float w = 1.0f / (1.0f + expf(-ig.wet[0]));
+  float tt[8], env[8], nz[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int64_t i = (int64_t)p * kP + j + 256 * r;
+    tt[r] = (float)i / ig.sr;
+    env[r] = expf((neg * tt[r]) * 500.0f);
+    nz[r] = i < ig.L ? ig.noise[i] : 0.0f;
+  }
+  fft4096<true>(v, lds);
+  const float inv_n = 1.0f / (float)kN;
+  double aw = 0.0, ad = 0.0;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int64_t i = (int64_t)p * kP + j + 256 * r;
+    const float di = v[r + 8].x * inv_n;
+    if (dimp && i < kc) dimp[i] = di;
+    if (i < ig.L) {
+      const float gi = (i >= 1 && i < kc) ? di : 0.0f;
+      ig.d_noise[i] = gi * env[r] * w;
+      const float gne = gi * nz[r] * env[r];
+      aw += (double)gne;
+      ad += (double)gne * (double)tt[r];
+    }
+  }
+  // taps past the partitions (an IR longer than the signal): no gradient
+  for (int64_t i = (int64_t)Qp * kP + (int64_t)p * kNT + j; i < ig.L; i += (int64_t)Qp * kNT) ig.d_noise[i] = 0.0f;
+  block_sum_double2(aw, ad, red);
+  if (j == 0) {
+    partials[2 * p] = aw;
+    partials[2 * p + 1] = ad;
+    __threadfence();
+    last = atomicAdd(arrivals, 1u) == (unsigned)(Qp - 1);
+  }
+  __syncthreads();
+  if (!last || j >= 64) return;
+  __threadfence();
+  double sw = 0.0, sd = 0.0;
+  for (int i = j; i < Qp; i += 64) {
+    sw += __hip_atomic_load(partials + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sd += __hip_atomic_load(partials + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sw += __shfl_down(sw, o, 64);
+    sd += __shfl_down(sd, o, 64);
+  }
+  if (j != 0) return;
+  const float spg = d > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-d));  // softplus'(d)
+  ig.d_wet[0] = (float)(sw * (double)w * (1.0 - (double)w));
+  ig.d_decay[0] = (float)(sd * (double)w * 500.0 * (double)spg);
+  *arrivals = 0u;
 }
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -761,20 +837,25 @@ size_t upols_spectra_bytes(int64_t rows, int64_t n) {
   return (size_t)npairs * upols_blocks(n) * kN * sizeof(float2);
 }
 
+static size_t impulse_scratch_bytes(int64_t Q) { return 256 + (((size_t)Q * 2 * sizeof(double) + 255) & ~(size_t)255); }
+
 size_t upols_backward_workspace_bytes(int64_t rows, int64_t n, int64_t klen, bool have_x) {
   const int64_t Q = upols_kernel_windows(std::min(klen, n));
   const int64_t groups = corr_groups((rows + 1) / 2);
-  return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)(groups + 1) * Q * kN * sizeof(float2);
+  // + the fused impulse gradient's partial sums and arrival counter (upols_corr_finish_impulse_kernel)
+  return (have_x ? 2 : 3) * upols_spectra_bytes(rows, n) + (size_t)(groups + 1) * Q * kN * sizeof(float2) +
+         impulse_scratch_bytes(Q);
 }
 
 int upols_backward(const float* x, const float* x_spectra, const float* spectrum, const float* g, int64_t rows,
-                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream) {
+                   int64_t n, int64_t klen, float* dx, float* dimp, void* ws, size_t ws_bytes, void* stream,
+                   const ImpulseGrad* ig) {
   const int64_t npairs = (rows + 1) / 2;
   const int64_t nb = upols_blocks(n);
   const int64_t kc = std::min(klen, n);
   const int64_t Qp = upols_partitions(kc), Q = Qp + 1;  // output partitions of dimp; kernel windows
   const int64_t groups = corr_groups(npairs);
-  const bool need_x = dimp && !x_spectra;
+  const bool need_x = (dimp || ig) && !x_spectra;
   if (!ws || ws_bytes < upols_backward_workspace_bytes(rows, n, klen, !need_x)) return DDSP_HIP_EWORKSPACE;
   if (nb > INT32_MAX || npairs > 65535 || Q > 65535 || (nb + kRingBlk - 1) / kRingBlk > 65535) return DDSP_HIP_EINVAL;
   const size_t sb = upols_spectra_bytes(rows, n);
@@ -782,7 +863,11 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
   float2* GZ = reinterpret_cast<float2*>(w);
   float2* V = reinterpret_cast<float2*>(w + sb);
   float2* part = reinterpret_cast<float2*>(w + 2 * sb);
-  float2* Xs = need_x ? reinterpret_cast<float2*>(w + 2 * sb + (size_t)(groups + 1) * Q * kN * sizeof(float2))
+  const bool want_imp = dimp || ig;
+  char* scratch = w + 2 * sb + (size_t)(groups + 1) * Q * kN * sizeof(float2);
+  unsigned* arrivals = reinterpret_cast<unsigned*>(scratch);
+  double* partials = reinterpret_cast<double*>(scratch + 256);
+  float2* Xs = need_x ? reinterpret_cast<float2*>(scratch + impulse_scratch_bytes(Q))
                       : const_cast<float2*>(reinterpret_cast<const float2*>(x_spectra));
   // GZ_b = F([0, g_b])
   int st = launch_forward(g, n, rows, 1, nb, npairs, -1, 1, 0, GZ, stream);
@@ -802,7 +887,7 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
                        (int)nb, n, (int)rows, 1, 0, dx, n);
     if ((st = launch_status())) return st;
   }
-  if (dimp) {
+  if (want_imp) {
     if (need_x) {
       if (!x) return DDSP_HIP_EINVAL;
       if ((st = launch_forward(x, n, rows, 1, nb, npairs, 0, 2, 0, Xs, stream))) return st;
@@ -820,9 +905,13 @@ int upols_backward(const float* x, const float* x_spectra, const float* spectrum
     if ((st = launch_status())) return st;
     float2* psum = part + (size_t)groups * Q * kN;
     hipLaunchKernelGGL(upols_corr_sum_kernel, dim3(kN / kNT, (unsigned)Qp), dim3(kNT), 0, S(stream), part,
-                       (int)groups, (int)Q, psum);
+                       (int)groups, (int)Q, psum, ig ? arrivals : nullptr);
     if ((st = launch_status())) return st;
-    hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), psum, kc, dimp);
+    if (ig)
+      hipLaunchKernelGGL(upols_corr_finish_impulse_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), psum, kc, *ig,
+                         partials, arrivals, dimp);
+    else
+      hipLaunchKernelGGL(upols_corr_finish_kernel, dim3((unsigned)Qp), dim3(kNT), 0, S(stream), psum, kc, dimp);
     if ((st = launch_status())) return st;
   }
   return DDSP_HIP_OK;

@@ -310,6 +310,22 @@ def reverb_backward(x, x_spectra, spectrum, g, ir_length, want_dx, want_dimp):
     return dx, dimp
 
 
+def reverb_backward_params(x_spectra, spectrum, g, noise, decay, wet, ir_length, sample_rate, want_dx):
+    """-> (dx or None, d_noise, d_decay, d_wet): reverb_backward + impulse_backward without the impulse
+    gradient round trip (csrc/upols.hip, upols_corr_finish_impulse_kernel)."""
+    B, T = g.shape[0], g.shape[1]
+    dx = torch.empty(B, T, 1, dtype=torch.float32, device=g.device) if want_dx else None
+    dn = torch.empty_like(core._c(noise))
+    dd = torch.empty((), dtype=torch.float32, device=g.device)
+    dw = torch.empty((), dtype=torch.float32, device=g.device)
+    ws = core._workspace(_lib.query("reverb_backward_workspace_size", B, T, int(ir_length), 1), g.device)
+    _lib.call("reverb_backward_params", _lib.ptr(None), _lib.ptr(x_spectra), _lib.ptr(spectrum), _lib.ptr(g),
+              _lib.ptr(core._c(noise)), _lib.ptr(core._c(decay)), _lib.ptr(core._c(wet)), float(sample_rate),
+              _lib.ptr(dx), _lib.ptr(dn), _lib.ptr(dd), _lib.ptr(dw), B, T, int(ir_length), _lib.ptr(ws), ws.numel(),
+              _lib.stream_of(g))
+    return dx, dn.reshape(noise.shape), dd.reshape(decay.shape), dw.reshape(wet.shape)
+
+
 def impulse_backward(noise, decay, wet, dimp, grad_length, sample_rate):
     L = noise.shape[0]
     dn = torch.empty_like(core._c(noise))
@@ -358,11 +374,12 @@ class ReverbFn(_F):
     def backward(ctx, g):
         noise, decay, wet = ctx.saved_tensors
         want_p = any(ctx.needs_input_grad[1:4])
-        dx, dimp = reverb_backward(None, ctx.ws, ctx.spectrum, _g(g), ctx.L, ctx.needs_input_grad[0], want_p)
         dn = dd = dw = None
-        if want_p:
-            dn, dd, dw = impulse_backward(noise.detach(), decay.detach(), wet.detach(), dimp, min(ctx.L, ctx.T),
-                                          ctx.sr)
+        if want_p:  # the impulse gradient never materialised (ddsp_hip_reverb_backward_params)
+            dx, dn, dd, dw = reverb_backward_params(ctx.ws, ctx.spectrum, _g(g), noise.detach(), decay.detach(),
+                                                    wet.detach(), ctx.L, ctx.sr, ctx.needs_input_grad[0])
+        else:
+            dx, _ = reverb_backward(None, None, ctx.spectrum, _g(g), ctx.L, True, False)
         ctx.ws = None
         return dx, dn, dd, dw, None, None, None
 

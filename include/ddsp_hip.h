@@ -424,6 +424,16 @@ size_t ddsp_hip_reverb_backward_workspace_size(int64_t batch, int64_t n_samples,
 int ddsp_hip_reverb_backward(const float* x, const float* input_spectra, const float* spectrum, const float* grad,
                              float* grad_x, float* grad_impulse, int64_t batch, int64_t n_samples,
                              int64_t ir_length, void* workspace, size_t workspace_bytes, void* stream);
+/* modules.py:21-35 Reverb.forward backward with respect to the signal AND the reverb's parameters in one call:
+ * ddsp_hip_reverb_backward's grad_x (nullable) and ddsp_hip_reverb_impulse_backward's grad_noise[ir_length],
+ * grad_decay, grad_wet (device scalars) from grad_impulse without materialising it — the partition
+ * transforms of the impulse gradient also apply build_impulse's backward and reduce the decay / wet sums
+ * (in a fixed order: deterministic).  Workspace: ddsp_hip_reverb_backward_workspace_size. */
+int ddsp_hip_reverb_backward_params(const float* x, const float* input_spectra, const float* spectrum, const float* grad,
+                                    const float* noise, const float* decay, const float* wet, float sample_rate,
+                                    float* grad_x, float* grad_noise, float* grad_decay, float* grad_wet, int64_t batch,
+                                    int64_t n_samples, int64_t ir_length, void* workspace, size_t workspace_bytes,
+                                    void* stream);
 size_t ddsp_hip_reverb_impulse_backward_workspace_size(int64_t length);
 int ddsp_hip_reverb_impulse_backward(const float* noise, const float* decay, const float* wet,
                                      const float* grad_impulse, int64_t length, int64_t grad_length,
