@@ -527,12 +527,29 @@ __global__ void __launch_bounds__(64 * kNvjpWaves) noise_vjp_wave_kernel(
   constexpr int n = 128, half = 64, NB = 65;
   extern __shared__ float4 smem_nv[];
   float* ct = reinterpret_cast<float*>(smem_nv);  // [n]
-  fill_cos_table(ct, n);
-  __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t frame = (int64_t)blockIdx.x * kNvjpWaves + wave;
-  if (frame >= frames) return;
   const int L = bs >> 3, Sg = nvjp_gstride(L), Sx = nvjp_xstride(L);
+  // the g windows' quads (<= 7 per lane at bs <= 1024) are loaded first: their HBM latency hides under the
+  // cosine table, the barrier and the Philox noise
+  const float* gf = grad + (frame < frames ? frame : 0) * bs;
+  const int wq = (L + 72) >> 2;  // quads per window
+  float4 gq[7];
+  int gdst[7];  // the quad's float offset in the window copies (-1: none)
+  const float rwq = 1.0f / (float)wq;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const int i = lane + 64 * r;
+    int s = (int)((float)i * rwq);  // i / wq (i < 512: the float quotient is within one of it)
+    s += (s + 1) * wq <= i;
+    s -= s * wq > i;
+    const int u = s * L + 4 * (i - s * wq);
+    gdst[r] = i < 8 * wq ? s * Sg + (u - s * L) : -1;
+    gq[r] = (i < 8 * wq && u < bs) ? *reinterpret_cast<const float4*>(gf + u) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  fill_cos_table(ct, n);
+  __syncthreads();
+  if (frame >= frames) return;
   float* gc = ct + n + wave * nvjp_wave_floats(bs);  // [8][Sg] window copies of g (zero past bs)
   float* xc = gc + 8 * Sg;                           // [8][Sx] the noise, one run per lag segment
   float* es = xc + 8 * Sx;                           // [128] e, then [64] s
@@ -541,14 +558,7 @@ __global__ void __launch_bounds__(64 * kNvjpWaves) noise_vjp_wave_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
-  // ---- loads: the 8 windows of g (the upstream gradient of the frame) and the frame's noise ----
-  const float* gf = grad + frame * bs;
-  const int wq = (L + 72) >> 2;  // quads per window
-  for (int i = lane; i < 8 * wq; i += 64) {
-    const int s = i / wq, u = s * L + 4 * (i - s * wq);
-    const float4 v = u < bs ? *reinterpret_cast<const float4*>(gf + u) : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(gc + s * Sg + (u - s * L)) = v;
-  }
+  // ---- the frame's noise, then the 8 windows of g (the upstream gradient of the frame) ----
   const int quads = bs >> 2;
   for (int t = lane; t < quads; t += 64) {
     float4 v;
@@ -562,6 +572,9 @@ __global__ void __launch_bounds__(64 * kNvjpWaves) noise_vjp_wave_kernel(
     const int s = (4 * t) / L;
     *reinterpret_cast<float4*>(xc + s * Sx + (4 * t - s * L)) = v;
   }
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+    if (gdst[r] >= 0) *reinterpret_cast<float4*>(gc + gdst[r]) = gq[r];
   wsync();
 
   // ---- correlation ----
