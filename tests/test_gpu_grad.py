@@ -142,7 +142,11 @@ def test_harmonic_module_grad(dd, B, F, bs, H):
     assert relerr(pg2.grad, pc.grad) < GRAD_REL, relerr(pg2.grad, pc.grad)
 
 
-@pytest.mark.parametrize("B,F,bs,NB", [(2, 16, 512, 65), (1, 8, 256, 65), (2, 4, 64, 17)])
+@pytest.mark.parametrize("B,F,bs,NB", [(2, 16, 512, 65), (1, 8, 256, 65), (2, 4, 64, 17),
+                                       # the wave-per-frame noise VJP's lag-segment tails (bs/8 = 80, 96, 112, 128
+                                       # lags: 64 + 16, 64 + 32, 64 + 32 + 16, 2 x 64) and a frame count that
+                                       # leaves its last workgroup partly empty
+                                       (1, 5, 640, 65), (1, 6, 768, 65), (1, 3, 896, 65), (2, 3, 1024, 65)])
 def test_noise_module_grad(dd, B, F, bs, NB):
     g = torch.Generator().manual_seed(4)
     mags = torch.randn(B, F, NB, generator=g)
