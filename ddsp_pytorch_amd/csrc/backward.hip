@@ -634,24 +634,54 @@ __global__ void __launch_bounds__(64 * kNvjpWaves) noise_vjp_wave_kernel(
   for (int o = 32; o > 0; o >>= 1) alt += __shfl_xor(alt, o, 64);
   wsync();
   float* sq = es + n;  // [64] s_q = e_q + e_{n-q} (q >= 1)
-  sq[lane] = lane ? eS + es[n - lane] : 0.0f;
+  // stored by parity: sq[(q & 1) * 32 + (q >> 1)]
+  sq[(lane & 1) * 32 + (lane >> 1)] = lane ? eS + es[n - lane] : 0.0f;
   wsync();
 
-  // ---- cosine transform: lane k < 64 ----
-  const int k = lane;
+  // ---- cosine transform, folded: c(q (64 - k)) = (-1)^q c(q k), so with E_k / O_k the even- / odd-q halves of
+  // sum_q s_q c(q k), dA'_k = E_k + O_k and dA'_{64-k} = E_k - O_k: lane l < 32 forms E_l, lane 32 + l forms O_l
+  // (32 terms each instead of 63), and E_32 = sum_j s_{2j} (-1)^j (O_32 = 0) comes from a wave sum ----
+  const int par = lane >> 5, kk = lane & 31;
+  const float* sp = sq + 32 * par;
+  const int step = (2 * kk) & (n - 1);
+  int idx = (par * kk) & (n - 1);  // (q k) mod n for q = 2 j + par, j = 0
   float v0 = 0.0f, v1 = 0.0f;
 #pragma unroll
-  for (int q4 = 0; q4 < 16; ++q4) {
-    const float4 s4 = *reinterpret_cast<const float4*>(sq + 4 * q4);
-    const float c0 = ct[(k * (4 * q4)) & (n - 1)], c1 = ct[(k * (4 * q4 + 1)) & (n - 1)];
-    const float c2 = ct[(k * (4 * q4 + 2)) & (n - 1)], c3 = ct[(k * (4 * q4 + 3)) & (n - 1)];
+  for (int j4 = 0; j4 < 8; ++j4) {
+    const float4 s4 = *reinterpret_cast<const float4*>(sp + 4 * j4);
+    const float c0 = ct[idx];
+    idx = (idx + step) & (n - 1);
+    const float c1 = ct[idx];
+    idx = (idx + step) & (n - 1);
+    const float c2 = ct[idx];
+    idx = (idx + step) & (n - 1);
+    const float c3 = ct[idx];
+    idx = (idx + step) & (n - 1);
     v0 = fmaf(s4.x, c0, v0);  // (s_0 = 0)
     v1 = fmaf(s4.y, c1, v1);
     v0 = fmaf(s4.z, c2, v0);
     v1 = fmaf(s4.w, c3, v1);
   }
+  const float half_sum = v0 + v1;                          // E_kk (par 0) or O_kk (par 1)
+  const float other = __shfl_xor(half_sum, 32, 64);        // the partner half
+  float e32 = par ? 0.0f : ((kk & 1) ? -sq[kk] : sq[kk]);  // s_{2 kk} (-1)^kk
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) e32 += __shfl_xor(e32, o, 64);  // within each 32-lane half
+  const float E32 = __shfl(e32, 0, 64);  // (a wave op: every lane takes part)
+  int k;
+  float sum;
+  if (!par) {  // k = kk: E + O
+    k = kk;
+    sum = half_sum + other;
+  } else if (kk) {  // k = 64 - kk: E - O
+    k = half - kk;
+    sum = other - half_sum;
+  } else {  // k = 32: E_32 (O_32 = 0)
+    k = 32;
+    sum = E32;
+  }
   const float inv_n = 1.0f / (float)n;
-  float dA = (v0 + v1 + es[0] + ((k & 1) ? -es[half] : es[half])) * (k == 0 ? 1.0f : 2.0f) * inv_n;
+  float dA = (sum + es[0] + ((k & 1) ? -es[half] : es[half])) * (k == 0 ? 1.0f : 2.0f) * inv_n;
   if (k & 1) dA = -dA;
   float* dm = d_mags + frame * NB;
   const float* mg = RAW ? mags + frame * NB : nullptr;
