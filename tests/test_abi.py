@@ -113,6 +113,11 @@ def test_training_entry_points_reject_bad_arguments_without_launching():
                                               1, 2, 4, 65, 512, 48000.0, null) == EINVAL
     # reverb backward: nothing requested / workspace
     assert lib.ddsp_hip_reverb_backward(null, null, null, null, null, null, 1, 100, 10, null, 0, null) == EINVAL
+    # reverb backward with the parameters' gradients: parameter pointers missing, negative batch, bad rate
+    assert lib.ddsp_hip_reverb_backward_params(null, null, null, null, null, null, null, 48000.0, null, null, null,
+                                               null, 1, 100, 10, null, 0, null) == EINVAL
+    assert lib.ddsp_hip_reverb_backward_params(null, null, null, null, null, null, null, 0.0, null, null, null,
+                                               null, -1, 100, 10, null, 0, null) == EINVAL
     # STFT: sizes outside the kernel's range, padding longer than the signal
     assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 100, 25, null) == ERANGE
     assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 8192, 2048, null) == ERANGE
