@@ -112,6 +112,9 @@ def parse():
                    help="skip the full training step of train.py (DDSPDecoder + spectral loss + backward + Adam)")
     p.add_argument("--no-decoder-leg", action="store_true",
                    help="skip the full DDSPDecoder.forward leg (GRU/MLP + synthesis)")
+    p.add_argument("--no-realtime-leg", action="store_true",
+                   help="skip config 3's realtime leg (1024-sample calls through the HIP-graph stream)")
+    p.add_argument("--realtime-calls", type=int, default=400)
     p.add_argument("--cpu-batch", type=int, default=None, help="items in the CPU-baseline sample")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -444,6 +447,61 @@ def decoder_synthesis_leg(args, inp, dev, reps=50):
                         f"NB {args.bands}, reverb {args.reverb_length}) from a fixed GRU output: projections, "
                         "fused synthesis writing signal + harmonic + noise + control dicts, reverb; batch "
                         f"{B} x {F} frames, device noise"}
+
+
+def realtime_leg(dev, calls=400, warm=40):
+    """BASELINE config 3: the realtime stream at the shipped model size — DDSPDecoder(512, 64, 65, 48000, 256,
+    False) (config.yaml's decoder with block 256, no reverb, export.py:33-40's realtime forward), batch 1,
+    one 1024-sample call at a time as the ddsp~ host makes them (realtime/ddsp_tilde/ddsp_model.cpp:32-52:
+    host pitch/loudness in, host audio out, the GRU state carried between calls), through
+    realtime.RealtimeGraph (one HIP-graph replay per call).  Per call: p50 / p99 wall time from the host's
+    buffers to the host's audio, and the device time of one replay.  Realtime factor as the reference's
+    performance.py:28-34 computes it: samples per call / (mean call time x sample rate).  The GRU runs on
+    both routes (step kernels, one persistent launch); the faster by p50 is reported."""
+    from ddsp_pytorch_amd.decoder import DDSPDecoder
+    from ddsp_pytorch_amd.realtime import RealtimeGraph
+    N, sr, bs = 1024, 48000, 256
+    torch.manual_seed(0)
+    m = DDSPDecoder(512, 64, 65, sr, bs, False).to(dev).eval()
+    g = torch.Generator().manual_seed(3)
+    ins = [(80.0 * 10.0 ** torch.rand(1, N, 1, generator=g), torch.randn(1, N, 1, generator=g) - 2.0)
+           for _ in range(16)]
+    by_route = {}
+    for route in ("steps", "persistent"):
+        rt = RealtimeGraph(m, N, fused=True, gru_route=route)
+        lat = []
+        with torch.no_grad():
+            for i in range(warm + calls):
+                p, l = ins[i % len(ins)]
+                t0 = time.perf_counter()
+                y = rt(p, l)
+                if i >= warm:
+                    lat.append((time.perf_counter() - t0) * 1e3)
+            assert torch.isfinite(y).all()
+            pd, ld = ins[0][0].to(dev), ins[0][1].to(dev)
+            for _ in range(20):
+                rt(pd, ld)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(200):
+                rt(pd, ld)
+            e1.record()
+            torch.cuda.synchronize()
+        lat.sort()
+        mean = sum(lat) / len(lat)
+        by_route[route] = {"p50_ms": round(lat[len(lat) // 2], 4), "p99_ms": round(lat[int(0.99 * len(lat))], 4),
+                           "mean_ms": round(mean, 4), "device_ms_per_replay": round(e0.elapsed_time(e1) / 200, 4),
+                           "realtime_factor": round(N / (mean * 1e-3 * sr), 1),
+                           "gru_route_taken": rt.gru_route_taken}
+        del rt
+    best = min(by_route, key=lambda r: by_route[r]["p50_ms"])
+    b = by_route[best]
+    return {"value": b["realtime_factor"], "unit": "x realtime (performance.py:28-34)", "p50_ms": b["p50_ms"],
+            "p99_ms": b["p99_ms"], "device_ms_per_replay": b["device_ms_per_replay"], "gru_route": best,
+            "by_route": by_route, "budget_ms": round(N / sr * 1e3, 3), "calls_timed": calls,
+            "workload": "config 3: DDSPDecoder(hidden 512, H 64, NB 65, 48 kHz, block 256, no reverb), batch 1, "
+                        "1024-sample calls (4 frames) host -> HIP-graph replay -> host, GRU state carried, "
+                        "device noise; random-init weights, synthetic pitch/loudness"}
 
 
 def _sync(dev):
@@ -811,6 +869,9 @@ def main():
     if rank == 0 and not args.no_decoder_leg:
         result["decoder_forward"] = decoder_leg(args, inp, dev)
         result["decoder_synthesis"] = decoder_synthesis_leg(args, inp, dev)
+
+    if rank == 0 and not args.no_realtime_leg:
+        result["realtime"] = realtime_leg(dev, args.realtime_calls)
 
     if rank == 0 and not args.no_model_train_leg:
         result["model_train_step"] = model_train_leg(args, inp, dev)

@@ -554,10 +554,11 @@ def gru_supported(gru_module):
             g.hidden_size % 64 == 0 and g.hidden_size <= 4096)
 
 
-def gru(x, gru_module, h0=None):
+def gru(x, gru_module, h0=None, persistent_flags=0):
     """torch.nn.GRU(x, h0) forward (1 layer, batch_first) -> (out [B,T,H], h_T [1,B,H]): the input
-    projection for all steps as one GEMM, the recurrence on the gfx950 step kernel; under autograd
-    the backward (BPTT) runs on the step kernels too (grad.GRUFn)."""
+    projection for all steps as one GEMM, the recurrence on the gfx950 kernels (gru_layer_launch); under
+    autograd the backward (BPTT) runs on the step kernels too (grad.GRUFn).  ``persistent_flags``:
+    the persistent launch's test hooks (GRU_SPREAD, GRU_NO_MASK_CHECK, GRU_FORCE_ABORT; 0 in use)."""
     _dev(x)
     if not gru_supported(gru_module):
         raise RuntimeError("gru: one layer, batch_first, unidirectional, with bias and hidden % 64 == 0 expected")
@@ -571,26 +572,58 @@ def gru(x, gru_module, h0=None):
     out = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
     h_last = torch.empty(1, B, H, dtype=torch.float32, device=x.device)
     h0c = _c(h0.reshape(B, H)) if h0 is not None else None
-    gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, None)
+    gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, None, persistent_flags)
     return out, h_last
 
 
-def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates):
+# include/ddsp_hip.h: ddsp_hip_gru_forward_persistent's flags (test hooks) and status bits
+GRU_SPREAD, GRU_NO_MASK_CHECK, GRU_FORCE_ABORT = 1, 2, 4
+GRU_STATUS_LOCAL, GRU_STATUS_RESCUED = 1, 2
+_GRU_LAST = {}  # device index -> (route, persistent workspace or None) of the last gru_layer_launch
+
+
+def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates, persistent_flags=0):
     """The layer's forward on the device: the input projection for every step as one GEMM, then the
-    recurrence as one persistent launch (ddsp_hip_gru_forward_persistent, hidden 512 and batch <= 64) or
-    on ddsp_hip_gru_forward's step kernels (a form with each step's projection inside the step launch
-    measured slower: 13.3 vs 7.4-7.8 us per step)."""
+    recurrence as one persistent launch (ddsp_hip_gru_forward_persistent: hidden 512, batch <= 64, a stream
+    that may use every CU) or on ddsp_hip_gru_forward's step kernels (a form with each step's projection
+    inside the step launch measured slower: 13.3 vs 7.4-7.8 us per step).  A persistent launch
+    that cannot get its workgroups resident aborts and its outputs are recomputed, on the same stream, with
+    the step kernels' arithmetic (gru_rescue_kernel): the values are right on every route;
+    ``gru_last_route`` tells which one ran.  Returns the route taken ("persistent" or "steps")."""
     B, T, I = x.shape
     H = w_hh.shape[1]
     xp = torch.addmm(b_ih, _c(x).reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
     args = (_lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out), _lib.ptr(h_last),
             _lib.ptr(gates), B, T, H)
-    # hidden 512, batch <= 64: the whole recurrence as one persistent launch (W_hh resident in LDS, h handed
-    # between the workgroups of a group); otherwise (ERANGE) one launch per step
+    # hidden 512, batch <= 64: the whole recurrence as one persistent launch (W_hh resident in registers, h
+    # handed between the workgroups of a group); otherwise (ERANGE) one launch per step
     ws = _workspace(_lib.query("gru_persistent_workspace_size"), out.device)
-    st = _lib.call("gru_forward_persistent", *args, _lib.ptr(ws), ws.numel(), _lib.stream_of(out), allow=(ERANGE,))
+    st = _lib.call("gru_forward_persistent", *args, int(persistent_flags), _lib.ptr(ws), ws.numel(),
+                   _lib.stream_of(out), allow=(ERANGE,))
+    dev = out.device.index if out.device.index is not None else torch.cuda.current_device()
     if st == ERANGE:
         _lib.call("gru_forward", *args, _lib.stream_of(out))
+        _GRU_LAST[dev] = ("steps", None)
+        return "steps"
+    _GRU_LAST[dev] = ("persistent", ws)
+    return "persistent"
+
+
+def gru_last_route(device=None):
+    """Which recurrence the last gru_layer_launch on ``device`` ran, read after a device synchronize:
+    {"route": "persistent" | "steps" | None, "hand_off": "xcd_local" | "write_through" | None,
+    "rescued": bool (the persistent launch aborted and the rescue kernel produced the outputs)}."""
+    dev = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    route, ws = _GRU_LAST.get(dev, (None, None))
+    info = {"route": route, "hand_off": None, "rescued": False}
+    if ws is not None:
+        torch.cuda.synchronize(dev)
+        off = int(_lib.query("gru_persistent_status_offset"))
+        word = int(ws[off:off + 4].cpu().view(torch.int32)[0])
+        info["rescued"] = bool(word & GRU_STATUS_RESCUED)
+        if not info["rescued"]:
+            info["hand_off"] = "xcd_local" if word & GRU_STATUS_LOCAL else "write_through"
+    return info
 
 
 def mlp_block(x, linear, norm, act, out=None, extras=()):

@@ -187,8 +187,10 @@ constexpr int kPR = 3 * kPU;       // W_hh rows per slot
 constexpr int kPI = 8;             // items per group (batch <= kPG * kPI)
 constexpr int kPCounterStride = 32;  // uint32 words between counters (one 128-B line each)
 // sync words: [g * stride] step counter of group g; [(8 + x) * stride] arrivals on XCD x; [16 * stride] all
-// arrivals; [17 * stride] abort
-constexpr int kPSyncWords = 18 * kPCounterStride;
+// arrivals; [17 * stride] abort; [18 * stride] route status (DDSP_HIP_GRU_STATUS_* bits, include/ddsp_hip.h)
+constexpr int kPAbortWord = 17 * kPCounterStride;
+constexpr int kPStatusWord = 18 * kPCounterStride;
+constexpr int kPSyncWords = 19 * kPCounterStride;
 constexpr uint64_t kPSpinTicks = 20000000;  // 200 ms at the 100 MHz realtime clock: an abort, never a hang
 
 __device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int voff) {
@@ -227,16 +229,12 @@ __device__ __forceinline__ float dpp_sum8(float v) {
   return v;
 }
 
-// An aborted launch (a workgroup that could not be resident within kPSpinTicks, e.g. beside another
-// long-running kernel) must not leave plausible values behind: every workgroup that sees the abort fills
-// the outputs with NaN (grid-strided), so the failure propagates visibly instead of as garbage.
-__device__ void gru_persistent_poison(float* __restrict__ out, float* __restrict__ h_last, int B, int T) {
-  const float qnan = __int_as_float(0x7fc00000);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = i0; i < (int64_t)B * T * kPH; i += stride) out[i] = qnan;
-  if (h_last)
-    for (int64_t i = i0; i < (int64_t)B * kPH; i += stride) h_last[i] = qnan;
-}
+// An aborted launch (a workgroup that could not be resident within kPSpinTicks: beside another long-running
+// kernel, on a CU-masked stream, under GPU sharing) simply ends: every workgroup that sees the abort word
+// returns.  The outputs are then recomputed by gru_rescue_kernel, which the same call enqueues behind the
+// persistent launch and which does nothing unless the abort word is set — so the caller always gets the
+// step kernels' values (bit for bit), never NaN or a half-finished sequence, and stream order (not a race
+// between workgroups of one launch) decides which values survive.
 
 template <bool kLocal>
 __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp, const float* __restrict__ w_hh,
@@ -244,8 +242,7 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
                                                     float* __restrict__ h_last, float* __restrict__ save, int B, int T,
                                                     int g, int s, uint32_t* __restrict__ counter,
                                                     uint32_t* __restrict__ abort_word, __amdgpu_buffer_rsrc_t rout,
-                                                    float* hs, float (*part)[kPR][kPI], int* s_abort,
-                                                    float* __restrict__ out) {
+                                                    float* hs, float (*part)[kPR][kPI], int* s_abort) {
   constexpr int kStoreAux = kLocal ? 0 : 16;  // write-back into the XCD's L2, or write-through (sc1)
   const int nI = B > g ? (B - g + kPG - 1) / kPG : 0;  // items of this group
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -292,10 +289,7 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
     if (t > 0) {  // every slot of the group has published h_{t-1}
       if (tid == 0 && !wait_at_least(counter, (uint32_t)kPS * (uint32_t)t, abort_word)) *s_abort = 1;
       __syncthreads();
-      if (*s_abort) {
-        gru_persistent_poison(out, h_last, B, T);
-        return;
-      }
+      if (*s_abort) return;  // gru_rescue_kernel recomputes the outputs
     }
     // h_{t-1} of the group's items into LDS, once per step (zeros past nI)
     {
@@ -384,12 +378,12 @@ __global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* __restrict__ 
 __global__ void __launch_bounds__(512) gru_persistent_kernel(
     const float* __restrict__ xp, const float* __restrict__ w_hh, const float* __restrict__ b_hh,
     const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
-    int B, int T, uint32_t* __restrict__ sync) {
+    int B, int T, uint32_t* __restrict__ sync, int flags) {
   __shared__ __attribute__((aligned(16))) float hs[kPI * kPH];      // h_{t-1} of the group's items, 16 KB
   __shared__ __attribute__((aligned(16))) float part[8][kPR][kPI];  // per-wave k partials
   __shared__ int s_abort, s_local, s_slot, s_group;
   const int tid = threadIdx.x;
-  uint32_t* abort_word = sync + 17 * kPCounterStride;
+  uint32_t* abort_word = sync + kPAbortWord;
   // census: this workgroup's XCD and its ticket there, then every workgroup's arrival
   if (tid == 0) {
     uint32_t xcc;
@@ -400,12 +394,19 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
     // (the ticket's value is used: the XCD add has completed before the total add)
     __hip_atomic_fetch_add(sync + 16 * kPCounterStride, ticket < 0x7fffffffu ? 1u : 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+    if (flags & DDSP_HIP_GRU_FORCE_ABORT)  // test hook: the abort path without a residency failure
+      __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = wait_at_least(sync + 16 * kPCounterStride, (uint32_t)(kPG * kPS), abort_word);
-    int local = 1;
+    // a workgroup whose census completed on its first poll has not looked at the abort word yet
+    ok = ok && __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    int local = !(flags & DDSP_HIP_GRU_SPREAD);
     if (ok) {
       for (int x = 0; x < kPG; ++x)
         local &= __hip_atomic_load(sync + (kPG + x) * kPCounterStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                  (uint32_t)kPS;
+      if (blockIdx.x == 0)  // one writer: which hand-off the launch used
+        __hip_atomic_store(sync + kPStatusWord, local ? (uint32_t)DDSP_HIP_GRU_STATUS_LOCAL : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     s_abort = !ok;
     s_local = local;
@@ -413,10 +414,7 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
     s_slot = local ? (int)ticket : (int)(blockIdx.x / kPG);
   }
   __syncthreads();
-  if (s_abort) {
-    gru_persistent_poison(out, h_last, B, T);
-    return;
-  }
+  if (s_abort) return;  // gru_rescue_kernel recomputes the outputs
   const int g = s_group, s = s_slot;
   if (B <= g) return;  // the group has no items: nobody waits for it
   // out as a buffer resource: byte offsets (< 2^31, checked by the host) with cache-policy bits
@@ -424,10 +422,76 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
   uint32_t* counter = sync + g * kPCounterStride;
   if (s_local)
     gru_persistent_body<true>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
-                              &s_abort, out);
+                              &s_abort);
   else
     gru_persistent_body<false>(xp, w_hh, b_hh, h0, h_last, save, B, T, g, s, counter, abort_word, rout, hs, part,
-                               &s_abort, out);
+                               &s_abort);
+}
+
+// The persistent launch's rescue, enqueued right behind it on the same stream by every
+// ddsp_hip_gru_forward_persistent call: unless the launch aborted it returns at once (one launch of B
+// one-wave-instruction workgroups, ~2 us).  After an abort it recomputes out, h_last and gates with
+// gru_step_kernel<16, 32, 512>'s arithmetic in the same order — each 16-wide k chunk's fma chain, the
+// chunks summed in pairs, pairs of pairs, then over the 8 waves from zero — so the results equal the step
+// kernels' bit for bit.  One workgroup per item (no residency requirement: the items are independent);
+// a half-wave per W_hh row (lane c holds k chunk c, 64 contiguous bytes of the row), 16 rows per pass,
+// W_hh re-read from L2 every step: slow (a fallback), but never wrong.
+__global__ void __launch_bounds__(512) gru_rescue_kernel(const float* __restrict__ xp, const float* __restrict__ w_hh,
+                                                         const float* __restrict__ b_hh, const float* __restrict__ h0,
+                                                         float* __restrict__ out, float* __restrict__ h_last,
+                                                         float* __restrict__ save, int B, int T,
+                                                         uint32_t* __restrict__ sync) {
+  if (__hip_atomic_load(sync + kPAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  __shared__ __attribute__((aligned(16))) float hs[kPH];  // h_{t-1} of this item
+  __shared__ float rows[3 * kPH];                           // W_hh h_{t-1} per gate row
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int lane = tid & 63, c = lane & 31;  // k chunk c: [16 c, 16 c + 16)
+  const int half = tid >> 5;                 // 16 half-waves
+  float hp = h0 ? h0[(int64_t)b * kPH + tid] : 0.0f;  // this thread's unit in the epilogue
+  hs[tid] = hp;
+  const float br = b_hh[tid], bz = b_hh[kPH + tid], bn = b_hh[2 * kPH + tid];
+  const int64_t plane = (int64_t)B * T * kPH;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    for (int row = half; row < 3 * kPH; row += 16) {
+      const float* wrow = w_hh + (int64_t)row * kPH + 16 * c;
+      float a = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = *reinterpret_cast<const float4*>(wrow + 4 * q);
+        const float4 h = *reinterpret_cast<const float4*>(&hs[16 * c + 4 * q]);
+        a = fmaf(w.x, h.x, fmaf(w.y, h.y, fmaf(w.z, h.z, fmaf(w.w, h.w, a))));
+      }
+      // gru_step_kernel's lane exchanges (xor 16, then 32, over the wave's 4 k chunks) as xor 1, 2 here
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      float s = 0.0f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) s += __shfl(a, (lane & 32) + 4 * v, 64);  // over its 8 waves, in order
+      if (c == 0) rows[row] = s;
+    }
+    __syncthreads();
+    const float* xr = xp + ((int64_t)b * T + t) * 3 * kPH;
+    const float r = sigmoidf_(xr[tid] + (rows[tid] + br));
+    const float z = sigmoidf_(xr[kPH + tid] + (rows[kPH + tid] + bz));
+    const float hn = rows[2 * kPH + tid];
+    const float n = tanhf(xr[2 * kPH + tid] + r * (hn + bn));
+    hp = (1.0f - z) * n + z * hp;
+    const int64_t oi = ((int64_t)b * T + t) * kPH + tid;
+    out[oi] = hp;
+    if (save) {
+      save[oi] = r;
+      save[plane + oi] = z;
+      save[2 * plane + oi] = n;
+      save[3 * plane + oi] = hn + bn;
+    }
+    hs[tid] = hp;  // every read of h_{t-1} (the row pass) is behind the barrier above
+    __syncthreads();
+  }
+  if (h_last) h_last[(int64_t)b * kPH + tid] = hp;
+  if (b == 0 && tid == 0)
+    __hip_atomic_store(sync + kPStatusWord, (uint32_t)DDSP_HIP_GRU_STATUS_RESCUED, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -734,9 +798,12 @@ extern "C" {
 
 size_t ddsp_hip_gru_persistent_workspace_size(void) { return sizeof(uint32_t) * kPSyncWords; }
 
+size_t ddsp_hip_gru_persistent_status_offset(void) { return sizeof(uint32_t) * kPStatusWord; }
+
 int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                                     float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
+                                    int flags, void* workspace, size_t workspace_bytes, void* stream) {
+  if (flags & ~(DDSP_HIP_GRU_SPREAD | DDSP_HIP_GRU_NO_MASK_CHECK | DDSP_HIP_GRU_FORCE_ABORT)) return DDSP_HIP_EINVAL;
   if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
   if (batch == 0 || steps == 0) return DDSP_HIP_OK;
   if (!xp || !w_hh || !b_hh || !out) return DDSP_HIP_EINVAL;
@@ -749,19 +816,36 @@ int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const fl
                        reinterpret_cast<uintptr_t>(h0) | reinterpret_cast<uintptr_t>(h_last) |
                        reinterpret_cast<uintptr_t>(gates);
   if (al & 15) return DDSP_HIP_ERANGE;
-  // every workgroup of a group must be resident at once (one 110 KB-LDS workgroup per CU)
+  // h_T over h0 in place: the groups finish independently, and a rescue after one group's abort re-reads h0
+  if (h0 && h0 == h_last) return DDSP_HIP_ERANGE;
+  // every workgroup of a group must be resident at once (237 VGPRs x 8 waves: one workgroup per CU)
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return DDSP_HIP_ELAUNCH;
   if (cus < kPG * kPS) return DDSP_HIP_ERANGE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // a stream whose kernels cannot reach every CU (hipExtStreamCreateWithCUMask, e.g. this library's
+  // ddsp_hip_stream_create_cu_masked) cannot hold the grid: refuse up front rather than wait for the abort
+  if (!(flags & DDSP_HIP_GRU_NO_MASK_CHECK)) {
+    uint32_t mask[32] = {0};
+    const int words = (cus + 31) / 32;
+    if (words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, mask) == hipSuccess) {
+      int on = 0;
+      for (int c = 0; c < cus; ++c) on += (mask[c >> 5] >> (c & 31)) & 1u;
+      if (on < cus) return DDSP_HIP_ERANGE;
+    }
+  }
+  uint32_t* sync = reinterpret_cast<uint32_t*>(workspace);
   // the sync words are zeroed by a kernel of ours: a hipMemsetAsync captured into a HIP graph wrote
   // 0x5EE0B080 instead of 0 on every replay after the first (ROCm 7.2, tools/dbg_gru_graph.py)
-  hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, reinterpret_cast<uint32_t*>(workspace), kPSyncWords);
+  hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, sync, kPSyncWords);
   if (int r = launch_status()) return r;
   hipLaunchKernelGGL(gru_persistent_kernel, dim3(kPG * kPS), dim3(512), 0, st, xp, w_hh, b_hh, h0, out, h_last, gates,
-                     (int)batch, (int)steps, reinterpret_cast<uint32_t*>(workspace));
+                     (int)batch, (int)steps, sync, flags);
+  if (int r = launch_status()) return r;
+  hipLaunchKernelGGL(gru_rescue_kernel, dim3((unsigned)batch), dim3(512), 0, st, xp, w_hh, b_hh, h0, out, h_last, gates,
+                     (int)batch, (int)steps, sync);
   return launch_status();
 }
 

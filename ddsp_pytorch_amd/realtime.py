@@ -38,7 +38,7 @@ class RealtimeGraph:
     with memcpy)."""
 
     def __init__(self, model, call_samples=1024, mean_loudness=0.0, std_loudness=1.0,
-                 seed=0x5EEDDD5B, device=None, warmup=3, fused=True):
+                 seed=0x5EEDDD5B, device=None, warmup=3, fused=True, gru_route="steps"):
         device = torch.device(device) if device is not None else next(model.parameters()).device
         if device.type != "cuda":
             raise RuntimeError("RealtimeGraph: the model must be on a HIP device")
@@ -65,6 +65,10 @@ class RealtimeGraph:
         self._inp_h = torch.zeros(2, N, 1).pin_memory()
         self._out_h = torch.zeros(1, N, 1).pin_memory()
         self.fused = bool(fused)
+        if gru_route not in ("steps", "persistent"):
+            raise ValueError("RealtimeGraph: gru_route must be 'steps' or 'persistent'")
+        self.gru_route = gru_route  # the route requested; gru_route_taken: the one the graph holds
+        self.gru_route_taken = None
         if self.fused:
             self._setup_fused()
         self.graph = torch.cuda.CUDAGraph()
@@ -97,11 +101,16 @@ class RealtimeGraph:
         self._buf = {"y2f": z(Hd), "y2l": z(Hd), "y3f": z(Hd), "y3l": z(Hd), "xp": z(3 * Hd),
                      "gru": z(Hd), "y4": z(Hd), "y5": z(Hd), "y6": z(Hd),
                      "param": z(m.harmonic_proj.out_features), "mags": z(m.noise_proj.out_features),
-                     "f0": z(1), "loud": z(1)}
+                     "f0": z(1), "loud": z(1), "h_last": z(Hd)[:1]}
+        # the persistent recurrence's sync words (ddsp_hip_gru_forward_persistent), zeroed by the call itself
+        self._gru_ws = torch.zeros(int(core._lib.query("gru_persistent_workspace_size")), dtype=torch.uint8,
+                                   device=dev)
 
     def _forward_fused(self):
         """The same forward on ddsp_hip_dense_rows: decoder.py:43-68 + the projections
-        (decoder.py:107-114) in 7 launches, the GRU on its step kernel, then the synthesis."""
+        (decoder.py:107-114) in 7 launches, the GRU on its step kernels (``gru_route="steps"``: R launches)
+        or as one persistent launch (``"persistent"``: zeroing + persistent + rescue-check launches), then
+        the synthesis."""
         m, d, bs, b = self.model, self.model.decoder, self.block_size, self._buf
         R, dev = self.call_samples // bs, self.device
         di = core.dense_input
@@ -118,9 +127,17 @@ class RealtimeGraph:
         w_ih = _Linear(g.weight_ih_l0, g.bias_ih_l0, g.input_size, 3 * g.hidden_size)
         core.dense_rows([([di(b["y3f"], norm=f0m[7]), di(b["y3l"], norm=lm[7])], w_ih, b["xp"])], R, dev)
         cache = d.cache_gru
-        core._lib.call("gru_forward", core._lib.ptr(b["xp"]), core._lib.ptr(g.weight_hh_l0), core._lib.ptr(g.bias_hh_l0),
-                       core._lib.ptr(cache), core._lib.ptr(b["gru"]), core._lib.ptr(cache), None, 1, R,
-                       g.hidden_size, core._lib.stream_of(cache))
+        L = core._lib
+        args = (L.ptr(b["xp"]), L.ptr(g.weight_hh_l0), L.ptr(g.bias_hh_l0), L.ptr(cache), L.ptr(b["gru"]))
+        st = core.ERANGE
+        if self.gru_route == "persistent":  # h_T into its own buffer: the rescue kernel re-reads h0
+            st = L.call("gru_forward_persistent", *args, L.ptr(b["h_last"]), None, 1, R, g.hidden_size, 0,
+                        L.ptr(self._gru_ws), self._gru_ws.numel(), L.stream_of(cache), allow=(core.ERANGE,))
+            if st == 0:
+                cache.view(1, -1).copy_(b["h_last"])
+        if st == core.ERANGE:  # one launch per step, h_T written over h0 (the step kernels allow it)
+            L.call("gru_forward", *args, L.ptr(cache), None, 1, R, g.hidden_size, L.stream_of(cache))
+        self.gru_route_taken = "persistent" if st == 0 else "steps"
         # out_mlp(cat([gru_out, f0, loudness])) (decoder.py:68), then the projections
         core.dense_rows([([di(b["gru"]), di(b["f0"]), di(b["loud"])], om[0], b["y4"])], R, dev)
         core.dense_rows([([di(b["y4"], norm=om[1])], om[3], b["y5"])], R, dev)

@@ -293,19 +293,35 @@ int ddsp_hip_stack_rows(const float* w1, int64_t w1_ld, const float* b1, int64_t
  * are GEMMs of it against h_{t-1}), grad_h0[B,H] (nullable).  Workspace: *_workspace_size. */
 int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                          float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden, void* stream);
-/* The same forward as ONE persistent launch (hidden 512, batch <= 64, out < 2 GiB, >= 256 CUs; else
- * DDSP_HIP_ERANGE and the caller uses ddsp_hip_gru_forward): 8 groups of 32 workgroups, group g owning
- * items g, g + 8, ...; each workgroup keeps its 48 rows of W_hh in LDS for the whole sequence and the
- * group's slots hand h_t to each other through the output sequence (write-through stores, a per-group
- * counter).  Needs all 256 workgroups resident together (one per CU): launched on a stream whose kernels
- * cannot reach every CU, it ends after a bounded wait (200 ms) with out and h_last filled with NaN rather
- * than hang or leave plausible values.  Workspace:
- * ddsp_hip_gru_persistent_workspace_size() bytes (zeroed by the call, on the stream, by a kernel of its own:
- * the call stays capturable into a HIP graph). */
+/* The same forward as ONE persistent launch (hidden 512, batch <= 64, out < 2 GiB, >= 256 CUs, a stream
+ * whose kernels may use every CU, h_last != h0; else DDSP_HIP_ERANGE and the caller uses
+ * ddsp_hip_gru_forward, which allows h_T over h0 in place): 8 groups
+ * of 32 workgroups, group g owning items g, g + 8, ...; each workgroup keeps its 48 rows of W_hh in
+ * registers for the whole sequence and the group's slots hand h_t to each other through the output
+ * sequence (a per-group counter).  It needs all 256 workgroups resident together; when they are not (another
+ * long-running kernel beside it, GPU sharing) every wait ends within 200 ms, the launch aborts, and a rescue
+ * kernel that the call always enqueues behind it recomputes out, h_last and gates exactly as
+ * ddsp_hip_gru_forward does (bit for bit) — the outputs are right either way, and the abort is reported in
+ * the workspace's status word (below).  Workspace: ddsp_hip_gru_persistent_workspace_size() bytes (zeroed by
+ * the call, on the stream, by a kernel of its own: the call stays capturable into a HIP graph); after the
+ * stream has passed the call, the uint32 at byte offset ddsp_hip_gru_persistent_status_offset() holds
+ * DDSP_HIP_GRU_STATUS_LOCAL (the hand-off stayed inside each XCD's L2), 0 (the placement-independent
+ * write-through hand-off) or DDSP_HIP_GRU_STATUS_RESCUED (aborted, the outputs come from the rescue kernel).
+ * flags: 0, or test hooks — DDSP_HIP_GRU_SPREAD (use the placement-independent hand-off whatever the
+ * census finds), DDSP_HIP_GRU_NO_MASK_CHECK (launch on a CU-masked stream anyway: the abort path under a
+ * real residency failure), DDSP_HIP_GRU_FORCE_ABORT (abort at the census). */
+enum {
+  DDSP_HIP_GRU_SPREAD = 1,
+  DDSP_HIP_GRU_NO_MASK_CHECK = 2,
+  DDSP_HIP_GRU_FORCE_ABORT = 4,
+  DDSP_HIP_GRU_STATUS_LOCAL = 1,
+  DDSP_HIP_GRU_STATUS_RESCUED = 2
+};
 size_t ddsp_hip_gru_persistent_workspace_size(void);
+size_t ddsp_hip_gru_persistent_status_offset(void);
 int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                                     float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden,
-                                    void* workspace, size_t workspace_bytes, void* stream);
+                                    int flags, void* workspace, size_t workspace_bytes, void* stream);
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden);
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,

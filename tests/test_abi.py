@@ -133,3 +133,11 @@ def test_training_entry_points_reject_bad_arguments_without_launching():
     one = ctypes.c_void_p(16)  # non-null placeholders: the range check comes first
     assert lib.ddsp_hip_gru_forward(one, one, one, null, one, null, null, 1, 4, 96, null) == ERANGE
     assert lib.ddsp_hip_gru_backward(one, one, one, null, null, null, one, one, null, 1, 4, 64, null, 0, null) == EWS
+    # persistent GRU: unknown flags, then the range checks, before any HIP call
+    assert lib.ddsp_hip_gru_forward_persistent(one, one, one, null, one, null, null, 1, 4, 512, 8, one, 4096,
+                                               null) == EINVAL
+    assert lib.ddsp_hip_gru_forward_persistent(one, one, one, null, one, null, null, 65, 4, 512, 0, one, 4096,
+                                               null) == ERANGE
+    assert lib.ddsp_hip_gru_forward_persistent(one, one, one, null, one, null, null, 1, 4, 512, 0, one, 4,
+                                               null) == EWS
+    assert lib.ddsp_hip_gru_persistent_status_offset() + 4 <= lib.ddsp_hip_gru_persistent_workspace_size()

@@ -124,3 +124,100 @@ def test_gru_persistent_route(dd, monkeypatch, B, T, with_h0):
         assert relerr(out, ref_out) < 1e-5, relerr(out, ref_out)
         assert relerr(h, ref_h) < 1e-5
         assert torch.equal(out, outs[0][0]) and torch.equal(h, outs[0][1])
+
+
+def _step_route(dd, monkeypatch, fn):
+    """Run fn() with the persistent launch refused (ERANGE), i.e. on ddsp_hip_gru_forward's step kernels."""
+    real = dd._lib.call
+
+    def refuse(name, *a, **k):
+        if name == "gru_forward_persistent":
+            return dd.core.ERANGE
+        return real(name, *a, **k)
+    with monkeypatch.context() as m:
+        m.setattr(dd._lib, "call", refuse)
+        return fn()
+
+
+def _layer(dd, g, x, h0, flags, gates):
+    """gru_layer_launch with every output (out, h_last and, if gates, the training planes)."""
+    B, T, _ = x.shape
+    out = torch.empty(B, T, 512, device="cuda")
+    hl = torch.empty(B, 512, device="cuda")
+    gt = torch.empty(4, B, T, 512, device="cuda") if gates else None
+    route = dd.core.gru_layer_launch(x, g.weight_ih_l0, g.bias_ih_l0, g.weight_hh_l0, g.bias_hh_l0, h0, out, hl, gt,
+                                     flags)
+    return route, out, hl, gt
+
+
+@pytest.mark.parametrize("B,T,with_h0,gates", [(8, 16, False, False), (1, 4, True, True), (64, 9, True, True),
+                                               (3, 1, False, True)])
+def test_gru_persistent_abort_is_rescued_bit_exact(dd, monkeypatch, B, T, with_h0, gates):
+    """an aborted persistent launch must not hand back NaN.  GRU_FORCE_ABORT aborts it at the
+    census; the rescue kernel the call enqueues behind it recomputes out, h_last and the training planes
+    with the step kernels' arithmetic — equal to the step route bit for bit — and the status word says so."""
+    torch.manual_seed(B * 7 + T)
+    g = torch.nn.GRU(1024, 512, batch_first=True).cuda()
+    x = torch.randn(B, T, 1024, device="cuda")
+    h0 = torch.randn(B, 512, device="cuda") * 0.5 if with_h0 else None
+    with torch.no_grad():
+        route, out, hl, gt = _layer(dd, g, x, h0, dd.core.GRU_FORCE_ABORT, gates)
+        st = dd.core.gru_last_route()
+        ref = _step_route(dd, monkeypatch, lambda: _layer(dd, g, x, h0, 0, gates))
+    torch.cuda.synchronize()
+    assert route == "persistent" and st["rescued"], st
+    assert ref[0] == "steps"
+    assert torch.isfinite(out).all() and torch.isfinite(hl).all()
+    assert torch.equal(out, ref[1]) and torch.equal(hl, ref[2])
+    if gates:
+        assert torch.equal(gt, ref[3])
+    with torch.no_grad():
+        ref_out, ref_h = g.cpu()(x.cpu(), h0.cpu()[None] if with_h0 else None)
+    assert relerr(out, ref_out) < 1e-5 and relerr(hl, ref_h[0]) < 1e-5
+
+
+def test_gru_on_cu_masked_stream(dd, monkeypatch):
+    """VERDICT r05 #1's done-criterion: core.gru (hidden 512, B=8, T=16) on a 64-CU masked stream.  The
+    persistent route is refused up front (the stream cannot hold its grid) and the step kernels run; with
+    the up-front check disabled (GRU_NO_MASK_CHECK) the launch really cannot get its 256 workgroups
+    resident, aborts after its bounded wait and is rescued.  Both give the step route's values, never NaN."""
+    torch.manual_seed(11)
+    g = torch.nn.GRU(1024, 512, batch_first=True).cuda()
+    x = torch.randn(8, 16, 1024, device="cuda")
+    with torch.no_grad():
+        ref_out, ref_h = _step_route(dd, monkeypatch, lambda: dd.core.gru(x, g))
+        torch.cuda.synchronize()
+        s = dd.core.cu_masked_stream(range(64))
+        with torch.cuda.stream(s):
+            out, h = dd.core.gru(x, g)
+        s.synchronize()
+        st1 = dd.core.gru_last_route()
+        with torch.cuda.stream(s):
+            out2, h2 = dd.core.gru(x, g, persistent_flags=dd.core.GRU_NO_MASK_CHECK)
+        s.synchronize()
+        st2 = dd.core.gru_last_route()
+    assert st1["route"] == "steps", st1
+    assert st2["route"] == "persistent" and st2["rescued"], st2
+    for o, hh in ((out, h), (out2, h2)):
+        assert torch.isfinite(o).all() and torch.isfinite(hh).all()
+        assert torch.equal(o, ref_out) and torch.equal(hh, ref_h)
+
+
+def test_gru_persistent_write_through_hand_off(dd):
+    """the placement-independent hand-off (group = blockIdx % 8, write-through h) is the
+    correctness backstop for any placement; GRU_SPREAD forces it.  Same arithmetic per (item, unit) as the
+    XCD-local route, so the outputs are identical; the default route reports its XCD-local hand-off."""
+    torch.manual_seed(5)
+    g = torch.nn.GRU(1024, 512, batch_first=True).cuda()
+    x = torch.randn(20, 40, 1024, device="cuda")
+    h0 = torch.randn(1, 20, 512, device="cuda") * 0.5
+    with torch.no_grad():
+        a = dd.core.gru(x, g, h0)
+        sa = dd.core.gru_last_route()
+        b = dd.core.gru(x, g, h0, persistent_flags=dd.core.GRU_SPREAD)
+        sb = dd.core.gru_last_route()
+        ref_out, ref_h = g.cpu()(x.cpu(), h0.cpu())
+    assert sa == {"route": "persistent", "hand_off": "xcd_local", "rescued": False}, sa
+    assert sb == {"route": "persistent", "hand_off": "write_through", "rescued": False}, sb
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert relerr(b[0], ref_out) < 1e-5 and relerr(b[1], ref_h) < 1e-5

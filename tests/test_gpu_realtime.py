@@ -52,17 +52,20 @@ def test_realtime_graph_needs_device():
 
 
 @gpu
-@pytest.mark.parametrize("fused", [False, True])
-def test_realtime_graph_matches_eager_calls(fused):
+@pytest.mark.parametrize("fused,route", [(False, "steps"), (True, "steps"), (True, "persistent")])
+def test_realtime_graph_matches_eager_calls(fused, route):
     """fused=False replays the eager kernels (bit-equal); fused=True runs the control network on
-    ddsp_hip_dense_rows (different fp32 summation order: ≤1e-5 RMS on the audio)."""
+    ddsp_hip_dense_rows (different fp32 summation order: ≤1e-5 RMS on the audio), its GRU on the step
+    kernels or as one persistent launch (gru_route)."""
     from ddsp_pytorch_amd.realtime import RealtimeGraph
     from oracle import torch_ref as tr
     dev = torch.device("cuda", 0)
     mean, std, seed = -3.0, 1.5, 77
     mg = _model().to(dev)
     me = _model().to(dev)
-    rt = RealtimeGraph(mg, N, mean, std, seed=seed, fused=fused)
+    rt = RealtimeGraph(mg, N, mean, std, seed=seed, fused=fused, gru_route=route)
+    if fused:
+        assert rt.gru_route_taken == route
     with torch.no_grad():
         for k, (pitch, loud) in enumerate(_calls(5)):
             y = rt(pitch, loud).clone()

@@ -21,7 +21,7 @@ ws = torch.zeros(_lib.query("gru_persistent_workspace_size"), dtype=torch.uint8,
 
 def run():
     _lib.call("gru_forward_persistent", _lib.ptr(xp), _lib.ptr(w_hh), _lib.ptr(b_hh), _lib.ptr(h0), _lib.ptr(out),
-              _lib.ptr(hl), None, B, T, H, _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
+              _lib.ptr(hl), None, B, T, H, 0, _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
 
 
 def words():

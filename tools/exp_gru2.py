@@ -42,7 +42,7 @@ with torch.no_grad():
 
     def persistent():
         _lib.call("gru_forward_persistent", _lib.ptr(xp), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(out), None,
-                  None, B, T, H, _lib.ptr(ws), ws.numel(), st())
+                  None, B, T, H, 0, _lib.ptr(ws), ws.numel(), st())
     res = {"steps_ms": dev_ms(steps)}
     ref = out.clone()
     res["persistent_ms"] = dev_ms(persistent)
@@ -56,5 +56,5 @@ with torch.no_grad():
         ob = torch.empty(b, T, H, device="cuda")
         res[f"persistent_B{b}_ms"] = dev_ms(lambda: _lib.call(
             "gru_forward_persistent", _lib.ptr(xb), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(ob), None, None,
-            b, T, H, _lib.ptr(ws), ws.numel(), st()))
+            b, T, H, 0, _lib.ptr(ws), ws.numel(), st()))
 print(json.dumps(res), flush=True)

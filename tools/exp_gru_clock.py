@@ -18,7 +18,7 @@ out = torch.empty(B, T, H, device="cuda")
 ws = torch.zeros(_lib.query("gru_persistent_workspace_size"), dtype=torch.uint8, device="cuda")
 for _ in range(3):
     _lib.call("gru_forward_persistent", _lib.ptr(xp), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(out), None, None,
-              B, T, H, _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
+              B, T, H, 0, _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
 torch.cuda.synchronize()
 st = ws.view(torch.int32)[18 * 32:18 * 32 + 8 * T].view(T, 8)[:, :5].cpu().long()
 st = (st - st[0, 0]) * 10  # ns
