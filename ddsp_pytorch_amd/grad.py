@@ -363,8 +363,12 @@ class ReverbFn(_F):
         out, ws, spectrum = run(x)  # modules.Reverb._forward_cached: (out, workspace, spectrum of the cache)
         ctx.save_for_backward(noise, decay, wet)
         ctx.ws = ws if any(ctx.needs_input_grad[1:4]) else None
-        # the cache's spectrum is rebuilt in place only when noise / decay / wet change, which autograd
-        # refuses between this forward and its backward (they are saved tensors)
+        # a view of the module's cache, rebuilt in place by a later forward only if noise / decay / wet
+        # have changed by then.  In-place changes through autograd-visible ops are refused at backward
+        # (they are saved tensors, version-checked); a write through .data between this forward and its
+        # backward is not, and then the backward uses the new values — for the spectrum exactly as torch's
+        # own autograd does for every saved tensor so modified (the .data hazard of any torch module).
+        # Forwards on other streams are ordered with this one by Reverb._ir_cache.
         ctx.spectrum = spectrum
         ctx.T = x.shape[1]
         ctx.L, ctx.sr = int(ir_length), float(sample_rate)

@@ -50,15 +50,23 @@ class Reverb(nn.Module):
 
     def _ir_cache(self, n_samples):
         """The device IR cache for inputs of n_samples (one per device and length: the crop/pad of
-        modules.py:31-33 depends on it), zero-filled when new."""
+        modules.py:31-33 depends on it), zero-filled when new.  The launch that validates it may rewrite
+        it in place, so uses of one cache from different streams are ordered: a stream that takes the
+        cache over from another first waits for everything that stream has enqueued (its reads of the
+        spectrum included; synth.PipelinedSynthPath reads it on its reverb stream).  Same-stream use,
+        the common case, costs nothing."""
         caches = self.__dict__.setdefault("_ir_caches", {})
         key = (self.noise.device, int(n_samples), int(self.length))
-        c = caches.get(key)
-        if c is None:
+        entry = caches.get(key)
+        if entry is None:
             c = torch.zeros(core.reverb_cache_bytes(n_samples, self.length), dtype=torch.uint8,
                             device=self.noise.device)
-            caches[key] = c
-        return c
+            entry = caches[key] = [c, torch.cuda.current_stream(c.device)]
+        cur = torch.cuda.current_stream(entry[0].device)
+        if cur != entry[1]:
+            cur.wait_stream(entry[1])
+            entry[1] = cur
+        return entry[0]
 
     def _forward_cached(self, x):
         """-> (out, workspace, spectrum): the reverb with the validated device cache (one launch group)."""

@@ -158,7 +158,11 @@ int ddsp_hip_synth_frames_controls(const float* f0, const float* param, int64_t 
  * reference's cumsum, core.py:138, at each frame's start), as ddsp_hip_frame_phase_prefix writes it.
  * Without it every frame's workgroup sums its earlier frames itself: O(frames) per frame, O(frames^2)
  * per item — the right choice for a few hundred frames, not for a minute of audio (5,625 frames at
- * block 512).  Every partial sum is exact in fp64, so both give the same bits. */
+ * block 512).  Both routes give the same bits wherever every partial sum is exact in fp64, i.e. while the
+ * increments' significant bits together with log2(frames * block_size) span <= 53 bits (f0 of audio pitch,
+ * tests/test_gpu_long_render.py); near-zero f0 (unvoiced frames, increments with ulps far below the running
+ * sum's) rounds the sums and the two summation orders may differ in the phase's last bits — inside the
+ * sine's 1e-6 tolerance, and checked at that tolerance. */
 int ddsp_hip_synth_frames_controls_prefix(const float* f0, const float* param, int64_t param_ld,
                                           const float* raw_magnitudes, int64_t magnitudes_ld, float bias,
                                           const float* noise, uint64_t seed, uint64_t offset, float* out,

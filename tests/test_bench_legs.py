@@ -111,3 +111,82 @@ def test_bench_n_gt_1_legs_gloo_world2():
             assert d["unit"] == "samples/s" and d["value"] > 0 and d["ms_per_step"] > 0
             assert "gloo" in d["collective"]
     assert out[0]["r2"]["chunks"] == 2 and out[0]["r5"]["value"] > 0
+
+
+def _world8_worker(rank, world, port, q):
+    """Config-5-shaped items at the target world size (8 GPUs of one node): H=128, NB=65,
+    bs=512, F reduced to 40, a ragged global batch of 61 (7 or 8 items per rank), 4 chunks.  Runs bench's
+    two N>1 legs and the pipelined path with its event trace."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        import bench
+        from ddsp_pytorch_amd.shard import shard, synthesize_pipelined
+        from ddsp_pytorch_amd.synth import make_inputs
+        cpu = torch.device("cpu")
+        batch, F, H, NB, bs = 61, 40, 128, 65, 512
+        inp = make_inputs(batch, F, H, NB, bs, seed=7, with_noise=False)
+
+        def synth(f0, p, m):  # item-local, deterministic stand-in for the kernels (which cannot run here)
+            v = f0[:, :, 0] * 1e-3 + p.sum(-1) - m.mean(-1)
+            return (v.repeat_interleave(bs, 1) * torch.linspace(0.5, 1.0, bs).repeat(F)).unsqueeze(-1)
+
+        keys = ["f0", "param", "mags"]
+        tails = [tuple(inp[k].shape[1:]) for k in keys]
+        local = {k: shard(inp[k], rank, world) for k in keys}
+        sps = batch * F * bs
+        r1, g1 = bench.gathered_leg(lambda: synth(local["f0"], local["param"], local["mags"]), batch, sps, 2,
+                                    cpu, dist)
+        held = [inp[k] for k in keys] if rank == 0 else None
+        r2, g2 = bench.scatter_gather_leg(synth, held, batch, tails, sps, 2, 4, cpu, dist, warm=1)
+        trace = []
+        g3 = synthesize_pipelined(synth, held, batch, tails, chunks=4, trace=trace)
+        res = {"trace": trace, "r1": r1, "r2": r2, "n_local": int(local["f0"].shape[0])}
+        if rank == 0:
+            full = synth(*[inp[k] for k in keys])  # one process, the whole batch
+            res["equal"] = [bool(torch.equal(g, full)) for g in (g1, g2, g3)]
+            res["shape"] = tuple(g1.shape)
+        else:
+            res["none"] = g1 is None and g2 is None and g3 is None
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_legs_gloo_world8_config5_items():
+    """readiness at the target world size.  World 8 over gloo, config-5-shaped items,
+    ragged shards, 4 chunks: the gathered and the scatter/gather legs' audio equals a one-process run bit
+    for bit, and the pipelined overlap order holds on every rank (scatter(c+1) issued before synth(c), each
+    gather issued before the next synth, none waited before the last synth).  No 1 -> 8 GPU curve exists
+    until the driver's SCALE run; this is the code path, not its speed."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world8_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert out[0]["equal"] == [True, True, True] and out[0]["shape"] == (61, 40 * 512, 1)
+    assert all(out[r]["none"] for r in range(1, world))
+    assert sorted(out[r]["n_local"] for r in range(world)) == [7, 7, 7, 8, 8, 8, 8, 8]
+    for r in range(world):
+        tr = out[r]["trace"]
+        pos = {e: i for i, e in enumerate(tr)}
+        n = 4
+        assert len(pos) == 5 * n, tr
+        last_synth = pos[("synth", n - 1)]
+        for c in range(n):
+            assert pos[("scattered", c)] < pos[("synth", c)] < pos[("gather", c)] < pos[("gathered", c)]
+            if c + 1 < n:
+                assert pos[("scatter", c + 1)] < pos[("synth", c)]
+                assert pos[("gather", c)] < pos[("synth", c + 1)]
+            assert pos[("gathered", c)] > last_synth
+        for leg in ("r1", "r2"):
+            assert out[r][leg]["value"] > 0 and "gloo" in out[r][leg]["collective"]

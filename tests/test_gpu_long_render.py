@@ -2,7 +2,9 @@
 kernel reads every frame's phase prefix from one ddsp_hip_frame_phase_prefix launch instead of summing its
 earlier frames itself (O(F) per frame, O(F^2) per item).  The prefix is the reference's cumsum
 (core.py:138) at each frame's start, exact in fp64, so both routes give the same bits; the harmonic output
-at F = 4096 matches the numpy oracle (oracle/numpy_oracle.py)."""
+at F = 4096 matches the numpy oracle (oracle/numpy_oracle.py).  (Bit identity holds while every partial sum is
+exact in fp64 — audio pitch; near-zero f0 mixed in rounds the sums, and the routes are then held to a
+tolerance: test_prefix_route_near_zero_f0.)"""
 import numpy as np
 import pytest
 import torch
@@ -71,3 +73,27 @@ def test_long_render_vs_oracle(dd):
     assert rms(harm.cpu().numpy(), harm_ref) < 1e-6
     assert rms(nz.cpu().numpy(), noise_ref) < 1e-7
     assert rms(out.cpu().numpy(), harm_ref + noise_ref) < 1e-5
+
+
+def test_prefix_route_near_zero_f0(dd, monkeypatch):
+    """unvoiced frames (f0 near 0, down to 1e-30 Hz, and exact zeros) among audio-pitch frames: the
+    fp64 partial sums are no longer all exact, so the precomputed prefix and the per-frame sums may round
+    differently.  Both routes stay within 1e-6 RMS of each other and of the oracle on the harmonic part."""
+    from oracle import numpy_oracle as no
+    B, F, H, NB, bs = 2, 700, 16, 65, 512
+    f0, param, mags, noise = _inputs(B, F, H, NB, bs, 4)
+    rng = np.random.default_rng(9)
+    tiny = (10.0 ** rng.uniform(-30, -3, size=f0.shape)).astype(np.float32)
+    f0 = np.where(rng.random(f0.shape) < 0.4, tiny, f0).astype(np.float32)
+    f0[:, ::50] = 0.0
+    c = no.harmonic_get_controls(param[..., :1], param[..., 1:], f0, 48000)
+    harm_ref, _ = no.harmonic_forward(c["amplitudes"], c["harmonic_distribution"], f0, bs, 48000)
+    args = [torch.as_tensor(a).cuda() for a in (f0, param, mags)]
+    with torch.no_grad():
+        a = dd.core.synth_frames(*args, bs, 48000, noise=torch.as_tensor(noise).cuda(), parts=True)
+        monkeypatch.setattr(dd.core, "FRAME_PREFIX_MIN_FRAMES", 1 << 30)
+        b = dd.core.synth_frames(*args, bs, 48000, noise=torch.as_tensor(noise).cuda(), parts=True)
+    monkeypatch.undo()
+    assert F >= dd.core.FRAME_PREFIX_MIN_FRAMES  # a is the prefix route
+    assert rms(a[1].cpu().numpy(), b[1].cpu().numpy()) < 1e-6
+    assert rms(a[1].cpu().numpy(), harm_ref) < 1e-6 and rms(b[1].cpu().numpy(), harm_ref) < 1e-6
