@@ -14,6 +14,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 HIPFLAGS_synth := -fno-slp-vectorize
 HIPFLAGS_synth_frame := -fno-slp-vectorize
 HIPFLAGS_backward := -fno-slp-vectorize
+# packed f32 VALU beside MFMAs costs more than the scalar pair (MI355X_MICROARCH.md cycle constants)
+HIPFLAGS_dense := -fno-slp-vectorize
 OBJ := $(patsubst ddsp_pytorch_amd/csrc/%.hip,build/%.o,$(SRC))
 
 TORCH_DIR := $(shell python3 -c "import torch,os;print(os.path.dirname(torch.__file__))" 2>/dev/null)

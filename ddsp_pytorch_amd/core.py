@@ -626,9 +626,13 @@ def gru_last_route(device=None):
     return info
 
 
-def mlp_block(x, linear, norm, act, out=None, extras=()):
+MLP_EXACT_F32 = 1  # include/ddsp_hip.h DDSP_HIP_MLP_EXACT_F32
+
+
+def mlp_block(x, linear, norm, act, out=None, extras=(), flags=0):
     """ddsp/core.py:122-129, one whole block: LeakyReLU(LayerNorm(linear(x))) in one launch
-    (ddsp_hip_mlp_block: the Linear on the fp32 matrix cores, LayerNorm + LeakyReLU in its epilogue).
+    (ddsp_hip_mlp_block: the Linear on the matrix cores — at 512 inputs fp32-accurate bf16x3 products,
+    ``flags=MLP_EXACT_F32`` the f32-input MFMA — LayerNorm + LeakyReLU in its epilogue).
     ``extras``: up to two [..., 1] tensors that are the Linear's LAST input features (the decoder's
     out_mlp input [gru_out, f0, loudness], decoder.py:68, given as x = gru_out, extras = (f0, loudness)).
     Returns None where the kernel does not apply (it is built for 512 output features);
@@ -652,7 +656,7 @@ def mlp_block(x, linear, norm, act, out=None, extras=()):
     st = _lib.call("mlp_block", _lib.ptr(xc), K, K, _lib.ptr(_c(linear.weight)), n_in, _lib.ptr(_c(linear.bias)),
                    _lib.ptr(ec[0] if ec else None), _lib.ptr(ec[1] if len(ec) > 1 else None), 1,
                    _lib.ptr(_c(norm.weight)), _lib.ptr(_c(norm.bias)), float(norm.eps), float(act.negative_slope),
-                   _lib.ptr(out), int(y_ld), int(rows), n_out, _lib.stream_of(out), allow=(ERANGE,))
+                   _lib.ptr(out), int(y_ld), int(rows), n_out, int(flags), _lib.stream_of(out), allow=(ERANGE,))
     return None if st == ERANGE else out
 
 

@@ -256,6 +256,91 @@ constexpr int kMlpKC = 32;          // K per LDS stage
 constexpr int kMlpLd = kMlpKC + 4;  // LDS row stride (floats): 16-B aligned rows, banks spread
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
+// The block's epilogue (both forms below): bias, the out_mlp's two extra input columns, LayerNorm (two-pass
+// mean / biased variance over the row, reduced across the 8 waves in LDS) and LeakyReLU, one store per value.
+__device__ __forceinline__ void mlp_epilogue(f32x4_t (&acc)[4][4], int64_t r0, int K, const float* __restrict__ w,
+                                             int64_t w_ld, const float* __restrict__ bias,
+                                             const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
+                                             const float* __restrict__ gamma, const float* __restrict__ beta,
+                                             float eps, float slope, float* __restrict__ y, int64_t y_ld, int64_t R,
+                                             float (*red)[kMlpRows], float* stat) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  // epilogue: acc[i][j][e] is row 16 i + 4 q + e, column 64 wv + 16 j + l16
+  float cb[4], cw0[4], cw1[4], cg[4], cbt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = 64 * wv + 16 * j + l16;
+    cb[j] = bias[col];
+    cw0[j] = e0 ? w[(int64_t)col * w_ld + K] : 0.0f;
+    cw1[j] = e1 ? w[(int64_t)col * w_ld + K + 1] : 0.0f;
+    cg[j] = gamma[col];
+    cbt[j] = beta[col];
+  }
+  float v[4][4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 16 * i + 4 * q + e;
+      const bool ok = row < R;
+      const float x0 = (e0 && ok) ? e0[row * e_ld] : 0.0f, x1 = (e1 && ok) ? e1[row * e_ld] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float h = acc[i][j][e] + cb[j];
+        if (e0) h += x0 * cw0[j];
+        if (e1) h += x1 * cw1[j];
+        v[i][j][e] = h;
+      }
+    }
+  // row means, then the biased variance about them (two passes, as accurate as torch's Welford)
+  auto row_reduce = [&](auto&& term) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += term(i, j, e);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the 16 lanes of one row
+        if (l16 == 0) red[wv][16 * i + 4 * q + e] = sum;
+      }
+    __syncthreads();
+    if (t < kMlpRows) {
+      float sum = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += red[k][t];
+      stat[t] = sum * (1.0f / (float)kMlpN);
+    }
+    __syncthreads();
+  };
+  row_reduce([&](int i, int j, int e) { return v[i][j][e]; });
+  float mean[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mean[i][e] = stat[16 * i + 4 * q + e];
+  row_reduce([&](int i, int j, int e) {
+    const float d = v[i][j][e] - mean[i][e];
+    return d * d;
+  });
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 16 * i + 4 * q + e;
+      if (row >= R) continue;
+      const float rstd = 1.0f / sqrtf(stat[16 * i + 4 * q + e] + eps);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float o = (v[i][j][e] - mean[i][e]) * rstd * cg[j] + cbt[j];
+        o = o >= 0.0f ? o : o * slope;
+        y[row * y_ld + 64 * wv + 16 * j + l16] = o;
+      }
+    }
+}
+
 template <int kVec>
 __global__ void __launch_bounds__(512) mlp_block_kernel(
     const float* __restrict__ x, int64_t x_ld, int K, const float* __restrict__ w, int64_t w_ld,
@@ -339,79 +424,250 @@ __global__ void __launch_bounds__(512) mlp_block_kernel(
       }
     }
   }
-  // epilogue: acc[i][j][e] is row 16 i + 4 q + e, column 64 wv + 16 j + l16
-  float cb[4], cw0[4], cw1[4], cg[4], cbt[4];
+  mlp_epilogue(acc, r0, K, w, w_ld, bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, R, red, stat);
+}
+
+// The same block with the x tile RESIDENT in LDS and W streamed straight into MFMA operand registers (the
+// decoder's blocks: K = 512).  Why: in the staged form above every K step is a pair of workgroup barriers
+// around one LDS stage that all 8 waves fill and then read, so the matrix pipe idles for the barrier, the
+// LDS writes and the first reads of every step (89 us per config-2 block against ~55 us of MFMA issue).
+// Here the workgroup's 64 x K slice of x is loaded into LDS once (133 KB at K = 512, rows padded to
+// K + 8 floats: the 16-lane groups of a ds_read_b128 then hit 16 distinct bank quads), and W needs no
+// LDS at all — wave wv alone uses output columns [64 wv, 64 wv + 64), so each lane loads its B fragment
+// (column 64 wv + 16 j + l16, k = 16 h + 4 q .. + 3: one float4 per tile and 16-wide K chunk h) from
+// global memory kP chunks ahead of its use into a register ring.  The main loop has no barrier: each wave
+// runs 4 LDS reads + 4 global loads + 64 MFMAs per chunk on its own.  Same operands per MFMA and the same
+// k order as the staged form (k = 16 h + 4 q + s at sub-step s), so the results are identical bit for bit.
+constexpr int kMlpResK = 512;
+constexpr int kMlpResLd = kMlpResK + 8;
+template <int kP>
+__global__ void __launch_bounds__(512) mlp_block_res_kernel(
+    const float* __restrict__ x, int64_t x_ld, const float* __restrict__ w, int64_t w_ld,
+    const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float slope, float* __restrict__ y,
+    int64_t y_ld, int64_t R) {
+  constexpr int K = kMlpResK, NH = K / 16;
+  static_assert(NH % kP == 0, "ring");
+  __shared__ __attribute__((aligned(16))) float xs[kMlpRows * kMlpResLd];
+  __shared__ float red[8][kMlpRows];
+  __shared__ float stat[kMlpRows];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
+  // this lane's W fragment rows: column 64 wv + 16 j + l16, k offset 4 q
+  const float* wl = w + (int64_t)(64 * wv + l16) * w_ld + 4 * q;
+  const int64_t wj = 16 * w_ld;
+  float4 wb[kP][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = 64 * wv + 16 * j + l16;
-    cb[j] = bias[col];
-    cw0[j] = e0 ? w[(int64_t)col * w_ld + K] : 0.0f;
-    cw1[j] = e1 ? w[(int64_t)col * w_ld + K + 1] : 0.0f;
-    cg[j] = gamma[col];
-    cbt[j] = beta[col];
+  for (int p = 0; p < kP; ++p)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wb[p][j] = *reinterpret_cast<const float4*>(wl + j * wj + 16 * p);
+  // the x tile into LDS (rows >= R read row R - 1: loaded, never stored)
+  {
+    constexpr int kF4 = kMlpRows * K / 4 / 512;  // float4 per thread
+    float4 v[kF4];
+#pragma unroll
+    for (int i = 0; i < kF4; ++i) {
+      const int f = t + 512 * i, row = f / (K / 4), c4 = f - row * (K / 4);
+      const int64_t rr = r0 + row < R ? r0 + row : R - 1;
+      v[i] = *reinterpret_cast<const float4*>(x + rr * x_ld + 4 * c4);
+    }
+#pragma unroll
+    for (int i = 0; i < kF4; ++i) {
+      const int f = t + 512 * i, row = f / (K / 4), c4 = f - row * (K / 4);
+      *reinterpret_cast<float4*>(&xs[row * kMlpResLd + 4 * c4]) = v[i];
+    }
   }
-  float v[4][4][4];
+  __syncthreads();
+  f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t row = r0 + 16 * i + 4 * q + e;
-      const bool ok = row < R;
-      const float x0 = (e0 && ok) ? e0[row * e_ld] : 0.0f, x1 = (e1 && ok) ? e1[row * e_ld] : 0.0f;
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const float* xl = xs + l16 * kMlpResLd + 4 * q;
+  for (int h0 = 0; h0 < NH; h0 += kP) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float h = acc[i][j][e] + cb[j];
-        if (e0) h += x0 * cw0[j];
-        if (e1) h += x1 * cw1[j];
-        v[i][j][e] = h;
+    for (int p = 0; p < kP; ++p) {
+      const int h = h0 + p;
+      float4 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const float4*>(xl + 16 * i * kMlpResLd + 16 * h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = s == 0 ? af[i].x : s == 1 ? af[i].y : s == 2 ? af[i].z : af[i].w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float b = s == 0 ? wb[p][j].x : s == 1 ? wb[p][j].y : s == 2 ? wb[p][j].z : wb[p][j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+          }
+        }
       }
+      // refill this ring slot with chunk h + kP (clamped: the last kP reloads re-read the final chunk, so
+      // every iteration issues the same loads and the wait counts stay exact)
+      const int hn = h + kP < NH ? h + kP : NH - 1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wb[p][j] = *reinterpret_cast<const float4*>(wl + j * wj + 16 * hn);
+      __builtin_amdgcn_sched_barrier(0);  // keep the refill here (the scheduler would sink it to the slot's use)
     }
-  // row means, then the biased variance about them (two passes, as accurate as torch's Welford)
-  auto row_reduce = [&](auto&& term) {
+  }
+  mlp_epilogue(acc, r0, K, w, w_ld, bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, R, red, stat);
+}
+
+// The decoder's blocks (K = 512) on the bf16 matrix cores with fp32 accuracy.  The f32-input MFMA runs at
+// 1/16 of the bf16 rate, and the kernels above are bound by it (84-90 us per config-2 block: 74 TF on the
+// 200 CUs a 12,800-row batch fills, at the clock MFMA-dense loops hold).  Here both operands are split
+// exactly into three bf16 terms, v = hi + mid + lo (hi = v with its low 16 bits cleared, mid the same of
+// v - hi, lo = v - hi - mid: each term exact, 8 significant bits apiece, together all 24 of the fp32
+// significand), and each 16 x 16 x 32 product is the six MFMAs hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid
+// — every bf16 x bf16 product is exact in fp32; the dropped mid.lo, lo.mid, lo.lo terms are < 2^-16 x 2^-8
+// of the product: an fp32-accurate GEMM (not bit-identical to the f32 MFMA's fma chain) at 6/16 of its
+// matrix time.  The split is VALU work, which the MFMAs leave free for 8 of every 16 issue cycles:
+//   * x (shared by the 8 waves) is split ONCE per workgroup, a quarter of K (128) at a time, into three bf16
+//     planes in LDS (48 KB per quarter, two quarters resident, 16-byte quads XOR-swizzled by row so that the
+//     fragment reads and the split's writes are conflict-free); the next quarter's fp32 loads are in
+//     flight during the current quarter's MFMAs; one barrier per quarter;
+//   * W (each wave alone uses its 64 output columns) is split by its wave, streamed from global memory into
+//     a register ring kP 32-wide chunks ahead of its use (no LDS).
+// Fragments (v_mfma_f32_16x16x32_bf16): lane (q, l16) holds A[row l16][k = 8 q .. + 7] and
+// B[k = 8 q .. + 7][col l16]; C/D as the f32 form (row 4 q + e, col l16), so the epilogue is shared.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 8 floats -> their exact three-term bf16 split, packed as MFMA fragments (element e = value e)
+__device__ __forceinline__ void split_bf16x3(const float4& a, const float4& b, u32x4_t& hi, u32x4_t& mid,
+                                             u32x4_t& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h[8], m[8], l[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t u = __float_as_uint(v[e]);
+    h[e] = u & 0xffff0000u;
+    const float r1 = v[e] - __uint_as_float(h[e]);  // exact
+    m[e] = __float_as_uint(r1) & 0xffff0000u;
+    l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));  // exact, <= 8 significant bits
+  }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float sum = 0.0f;
+  for (int e = 0; e < 4; ++e) {  // element pairs: high halves, low element first
+    hi[e] = __builtin_amdgcn_perm(h[2 * e + 1], h[2 * e], 0x07060302u);
+    mid[e] = __builtin_amdgcn_perm(m[2 * e + 1], m[2 * e], 0x07060302u);
+    lo[e] = __builtin_amdgcn_perm(l[2 * e + 1], l[2 * e], 0x07060302u);
+  }
+}
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4_t& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+constexpr int kBf3QK = 128;                     // K per quarter (LDS split stage)
+constexpr int kBf3Plane = kMlpRows * kBf3QK;    // bf16 elements per plane (row-major, 256 B rows)
+
+template <int kP>
+__global__ void __launch_bounds__(512) mlp_block_bf3_kernel(
+    const float* __restrict__ x, int64_t x_ld, const float* __restrict__ w, int64_t w_ld,
+    const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float slope, float* __restrict__ y,
+    int64_t y_ld, int64_t R) {
+  constexpr int K = kMlpResK, NQ = K / kBf3QK, NC = kBf3QK / 32;  // quarters; 32-wide chunks per quarter
+  static_assert((NQ * NC) % kP == 0 && NC % kP == 0, "ring");
+  // [buffer][plane hi/mid/lo][row][128 k] bf16, quads (8 bf16) at position Q ^ (row & 15)
+  __shared__ __attribute__((aligned(16))) uint32_t xs[2 * 3 * kBf3Plane / 2];
+  __shared__ float red[8][kMlpRows];
+  __shared__ float stat[kMlpRows];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
+  // W fragment of this lane: column 64 wv + 16 j + l16, k = 32 h + 8 q .. + 7 (two float4)
+  const float* wl = w + (int64_t)(64 * wv + l16) * w_ld + 8 * q;
+  const int64_t wj = 16 * w_ld;
+  float4 wb[kP][4][2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sum += term(i, j, e);
+  for (int p = 0; p < kP; ++p)
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the 16 lanes of one row
-        if (l16 == 0) red[wv][16 * i + 4 * q + e] = sum;
-      }
-    __syncthreads();
-    if (t < kMlpRows) {
-      float sum = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sum += red[k][t];
-      stat[t] = sum * (1.0f / (float)kMlpN);
+    for (int j = 0; j < 4; ++j) {
+      wb[p][j][0] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * p);
+      wb[p][j][1] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * p + 4);
     }
-    __syncthreads();
+  // split role: thread -> row t >> 3, k 16 (t & 7) .. + 15 of a quarter (quads Q = 2 (t & 7), + 1)
+  const int srow = t >> 3, sq = 2 * (t & 7);
+  const float* xsrc = x + (r0 + srow < R ? r0 + srow : R - 1) * x_ld + 8 * sq;  // rows >= R: never stored
+  float4 xv[4];
+  auto load_quarter = [&](int qt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const float4*>(xsrc + kBf3QK * qt + 4 * i);
   };
-  row_reduce([&](int i, int j, int e) { return v[i][j][e]; });
-  float mean[4][4];
+  auto store_quarter = [&](int buf) {
+    u32x4_t hq[2], mq[2], lq[2];
+    split_bf16x3(xv[0], xv[1], hq[0], mq[0], lq[0]);
+    split_bf16x3(xv[2], xv[3], hq[1], mq[1], lq[1]);
+    uint32_t* base = xs + buf * (3 * kBf3Plane / 2) + srow * (kBf3QK / 2);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pos = 4 * ((sq + e) ^ (srow & 15));  // uint32 offset of the quad
+      *reinterpret_cast<u32x4_t*>(base + pos) = hq[e];
+      *reinterpret_cast<u32x4_t*>(base + kBf3Plane / 2 + pos) = mq[e];
+      *reinterpret_cast<u32x4_t*>(base + kBf3Plane + pos) = lq[e];
+    }
+  };
+  load_quarter(0);
+  store_quarter(0);
+  load_quarter(1);
+  store_quarter(1);
+  load_quarter(2);  // in flight under quarter 0
+  __syncthreads();
+  f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) mean[i][e] = stat[16 * i + 4 * q + e];
-  row_reduce([&](int i, int j, int e) {
-    const float d = v[i][j][e] - mean[i][e];
-    return d * d;
-  });
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int qt = 0; qt < NQ; ++qt) {
+    const uint32_t* xb = xs + (qt & 1) * (3 * kBf3Plane / 2) + l16 * (kBf3QK / 2);  // row 16 i + l16: row & 15 = l16
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int c0 = 0; c0 < NC; c0 += kP) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t row = r0 + 16 * i + 4 * q + e;
-      if (row >= R) continue;
-      const float rstd = 1.0f / sqrtf(stat[16 * i + 4 * q + e] + eps);
+      for (int p = 0; p < kP; ++p) {
+        const int c = c0 + p, h = qt * NC + c;
+        const int pos = 4 * ((4 * c + q) ^ l16);
+        u32x4_t xh[4], xm[4], xlo[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float o = (v[i][j][e] - mean[i][e]) * rstd * cg[j] + cbt[j];
-        o = o >= 0.0f ? o : o * slope;
-        y[row * y_ld + 64 * wv + 16 * j + l16] = o;
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t* r = xb + 16 * i * (kBf3QK / 2) + pos;
+          xh[i] = *reinterpret_cast<const u32x4_t*>(r);
+          xm[i] = *reinterpret_cast<const u32x4_t*>(r + kBf3Plane / 2);
+          xlo[i] = *reinterpret_cast<const u32x4_t*>(r + kBf3Plane);
+        }
+        const int hn = h + kP < NQ * NC ? h + kP : NQ * NC - 1;  // clamped: the same loads every iteration
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u32x4_t wh, wm, wlo;
+          split_bf16x3(wb[p][j][0], wb[p][j][1], wh, wm, wlo);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {  // small terms first
+            f32x4_t a = acc[i][j];
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wm), a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xlo[i]), as_bf16x8(wh), a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wlo), a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wh), a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wm), a, 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wh), a, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          wb[p][j][0] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * hn);
+          wb[p][j][1] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * hn + 4);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the refill here (the scheduler would sink it to its use)
       }
     }
+    if (qt + 1 < NQ) {
+      __syncthreads();  // buffer qt & 1 fully read; the previous quarter's split writes visible
+      if (qt + 2 < NQ) {
+        store_quarter(qt & 1);  // quarter qt + 2
+        if (qt + 3 < NQ) load_quarter(qt + 3);
+      }
+    }
+  }
+  mlp_epilogue(acc, r0, K, w, w_ld, bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, R, red, stat);
 }
 
 // The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
@@ -488,8 +744,9 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
 int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
                        const float* bias, const float* e0, const float* e1, int64_t e_ld, const float* gamma,
                        const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
-                       int64_t out_features, void* stream) {
+                       int64_t out_features, int flags, void* stream) {
   if (rows < 0 || in_features < 1 || !w || !bias || !gamma || !beta || (!e0 && e1)) return DDSP_HIP_EINVAL;
+  if (flags & ~DDSP_HIP_MLP_EXACT_F32) return DDSP_HIP_EINVAL;
   if (rows == 0) return DDSP_HIP_OK;
   const int64_t extra = e1 ? 2 : e0 ? 1 : 0;
   if (!x || !y || x_ld < in_features || w_ld < in_features + extra || y_ld < out_features || (extra && e_ld < 1))
@@ -501,7 +758,13 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
                                       : (x_ld % 2 == 0 && w_ld % 2 == 0 && (al & 7) == 0) ? 2 : 1;
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (vec == 4)
+  if (in_features == kMlpResK && vec == 4 && (flags & DDSP_HIP_MLP_EXACT_F32) == 0)  // the decoder's blocks
+    hipLaunchKernelGGL(mlp_block_bf3_kernel<2>, grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
+                       beta, eps, slope, y, y_ld, rows);
+  else if (in_features == kMlpResK && vec == 4)  // x resident, W streamed to registers, f32 MFMA
+    hipLaunchKernelGGL(mlp_block_res_kernel<4>, grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
+                       beta, eps, slope, y, y_ld, rows);
+  else if (vec == 4)
     hipLaunchKernelGGL(mlp_block_kernel<4>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
                        e_ld, gamma, beta, eps, slope, y, y_ld, rows);
   else if (vec == 2)

@@ -260,14 +260,20 @@ typedef struct ddsp_hip_dense_problem {
 int ddsp_hip_dense_rows(const ddsp_hip_dense_problem* problems, int n_problems, int64_t rows, void* stream);
 
 /* ddsp/core.py:122-129: one whole MLP block, y = LeakyReLU(LayerNorm(x W^T + b)), W [out, w_ld] the
- * nn.Linear weight, for out_features = 512 (else DDSP_HIP_ERANGE): the Linear on the fp32 matrix cores,
+ * nn.Linear weight, for out_features = 512 (else DDSP_HIP_ERANGE): the Linear on the matrix cores,
  * LayerNorm + LeakyReLU in its epilogue.  e0/e1 (nullable, per-row scalars at stride e_ld) add
  * e0[r] W[:, in] + e1[r] W[:, in + 1] — the decoder's out_mlp input [gru_out, f0, loudness]
- * (decoder.py:68) without the concatenation.  y [rows, y_ld] may be a column slice. */
+ * (decoder.py:68) without the concatenation.  y [rows, y_ld] may be a column slice.
+ * The Linear's arithmetic: at in_features 512 with 16-byte aligned rows (the decoder's blocks) both operands
+ * split exactly into three bf16 terms and summed as six bf16 products per term pair on the bf16 matrix
+ * cores — fp32-accurate (the dropped terms are ~2^-24 of each product), not the same bits as an fp32 fma
+ * chain; flags = DDSP_HIP_MLP_EXACT_F32 (or any other shape) takes the f32-input MFMA, whose sums are
+ * exactly k-ordered fp32 fma chains. */
+enum { DDSP_HIP_MLP_EXACT_F32 = 1 };
 int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
                        const float* bias, const float* e0, const float* e1, int64_t e_ld, const float* gamma,
                        const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
-                       int64_t out_features, void* stream);
+                       int64_t out_features, int flags, void* stream);
 /* ddsp/core.py:122-129 (one MLP block after its Linear, decoder.py:25-42): y = LeakyReLU(LayerNorm(h))
  * per row of cols features, h = x [rows, x_ld] or, with w1/b1 (a Linear with ONE input feature),
  * h = x[r] * w1 + b1 formed on the fly.  gamma/beta: the LayerNorm's affine; eps and the negative

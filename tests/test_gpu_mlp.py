@@ -127,3 +127,58 @@ def test_projections_read_live_parameters(dd):
         l1.bias.data.mul_(2.0)
         a1 = dd.core.projections(x, l1, l2)[0]
     torch.testing.assert_close(a1, 2 * a0, rtol=1e-6, atol=1e-6)
+
+
+def _mlp_block_raw(dd, x, x_ld, lin, ln, rows, e0=None, e1=None, flags=0):
+    """ddsp_hip_mlp_block on a raw [rows, x_ld] buffer (x_ld > K selects the staged, unaligned-load form)."""
+    L = dd._lib
+    y = torch.empty(rows, 512, device="cuda")
+    L.call("mlp_block", L.ptr(x), x_ld, 512, L.ptr(lin.weight), lin.weight.shape[1], L.ptr(lin.bias), L.ptr(e0),
+           L.ptr(e1), 1, L.ptr(ln.weight), L.ptr(ln.bias), float(ln.eps), 0.01, L.ptr(y), 512, rows, 512, flags,
+           L.stream_of(y))
+    return y
+
+
+@pytest.mark.parametrize("rows,extras", [(12800, False), (1000, True), (65, False), (1, True)])
+def test_mlp_block_resident_form_equals_staged_form(dd, rows, extras):
+    """K = 512 with MLP_EXACT_F32 runs the x-resident f32 kernel (x tile in LDS, W streamed to registers, no
+    barrier in the K loop); an x buffer with row stride 514 floats runs the staged kernel.  Same MFMA operands
+    in the same k order: identical outputs, bit for bit, incl. the out_mlp's two extra columns.  The default
+    (bf16x3) form matches torch at the same tolerance."""
+    torch.manual_seed(rows)
+    lin = torch.nn.Linear(514 if extras else 512, 512).cuda()
+    ln = torch.nn.LayerNorm(512).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+        wide = torch.randn(rows, 514, device="cuda") * 2.0
+        x = wide[:, :512].contiguous()
+        e0 = torch.randn(rows, 1, device="cuda") if extras else None
+        e1 = torch.randn(rows, 1, device="cuda") if extras else None
+        a = _mlp_block_raw(dd, x, 512, lin, ln, rows, e0, e1, flags=dd.core.MLP_EXACT_F32)
+        b = _mlp_block_raw(dd, wide, 514, lin, ln, rows, e0, e1)
+        c = _mlp_block_raw(dd, x, 512, lin, ln, rows, e0, e1)
+        ref_in = torch.cat([x, e0, e1], -1) if extras else x
+        ref = torch.nn.functional.leaky_relu(ln(lin(ref_in)), 0.01)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a, ref, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(c, ref, rtol=2e-5, atol=2e-5)
+
+
+def test_mlp_block_bf16x3_is_fp32_accurate(dd):
+    """The bf16x3 Linear (six exact bf16 products per operand pair) against an fp64 evaluation of the same
+    block: its error is of the f32-input MFMA's order (within 2x of it, RMS and max) — fp32-accurate."""
+    torch.manual_seed(7)
+    rows = 4096
+    lin = torch.nn.Linear(512, 512).cuda()
+    ln = torch.nn.LayerNorm(512).cuda()
+    with torch.no_grad():
+        x = torch.randn(rows, 512, device="cuda") * 3.0
+        f32 = _mlp_block_raw(dd, x, 512, lin, ln, rows, flags=dd.core.MLP_EXACT_F32)
+        bf3 = _mlp_block_raw(dd, x, 512, lin, ln, rows)
+        h = x.double() @ lin.weight.double().t() + lin.bias.double()
+        ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(
+            h, (512,), ln.weight.double(), ln.bias.double(), ln.eps), 0.01)
+    e32, e3 = (f32.double() - ref), (bf3.double() - ref)
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    assert rms(e3) < 2 * rms(e32) and float(e3.abs().max()) < 2 * float(e32.abs().max()), (rms(e3), rms(e32))
