@@ -230,6 +230,38 @@ __device__ __forceinline__ void group_sum_double2(double& a, double& b, double* 
   }
 }
 
+// The exact three-term bf16 split of fp32 operands for the bf16 matrix cores (csrc/dense.hip's MLP blocks,
+// csrc/gru.hip's persistent recurrence): v = hi + mid + lo with hi = v with its low 16 bits cleared, mid the
+// same of v - hi, lo = v - hi - mid — each subtraction exact, each term 8 significant bits, together all 24
+// of the fp32 significand; summed as the six products hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid (each
+// exact in fp32; the dropped ones are below 2^-24 of the product) a product of two splits is fp32-accurate.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 8 floats -> their exact three-term bf16 split, packed as MFMA fragments (element e = value e)
+__device__ __forceinline__ void split_bf16x3(const float4& a, const float4& b, u32x4_t& hi, u32x4_t& mid,
+                                             u32x4_t& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h[8], m[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t u = __float_as_uint(v[e]);
+    h[e] = u & 0xffff0000u;
+    const float r1 = v[e] - __uint_as_float(h[e]);  // exact
+    m[e] = __float_as_uint(r1) & 0xffff0000u;
+    l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));  // exact, <= 8 significant bits
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // element pairs: high halves, low element first
+    hi[e] = __builtin_amdgcn_perm(h[2 * e + 1], h[2 * e], 0x07060302u);
+    mid[e] = __builtin_amdgcn_perm(m[2 * e + 1], m[2 * e], 0x07060302u);
+    lo[e] = __builtin_amdgcn_perm(l[2 * e + 1], l[2 * e], 0x07060302u);
+  }
+}
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4_t& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DDSP_HIP_OK : DDSP_HIP_ELAUNCH;

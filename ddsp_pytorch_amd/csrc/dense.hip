@@ -254,7 +254,6 @@ constexpr int kMlpN = 512;          // output features (8 waves x 64)
 constexpr int kMlpRows = 64;        // rows per workgroup
 constexpr int kMlpKC = 32;          // K per LDS stage
 constexpr int kMlpLd = kMlpKC + 4;  // LDS row stride (floats): 16-B aligned rows, banks spread
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // The block's epilogue (both forms below): bias, the out_mlp's two extra input columns, LayerNorm (two-pass
 // mean / biased variance over the row, reduced across the 8 waves in LDS) and LeakyReLU, one store per value.
@@ -532,31 +531,7 @@ __global__ void __launch_bounds__(512) mlp_block_res_kernel(
 //     a register ring kP 32-wide chunks ahead of its use (no LDS).
 // Fragments (v_mfma_f32_16x16x32_bf16): lane (q, l16) holds A[row l16][k = 8 q .. + 7] and
 // B[k = 8 q .. + 7][col l16]; C/D as the f32 form (row 4 q + e, col l16), so the epilogue is shared.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-// 8 floats -> their exact three-term bf16 split, packed as MFMA fragments (element e = value e)
-__device__ __forceinline__ void split_bf16x3(const float4& a, const float4& b, u32x4_t& hi, u32x4_t& mid,
-                                             u32x4_t& lo) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t h[8], m[8], l[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t u = __float_as_uint(v[e]);
-    h[e] = u & 0xffff0000u;
-    const float r1 = v[e] - __uint_as_float(h[e]);  // exact
-    m[e] = __float_as_uint(r1) & 0xffff0000u;
-    l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));  // exact, <= 8 significant bits
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {  // element pairs: high halves, low element first
-    hi[e] = __builtin_amdgcn_perm(h[2 * e + 1], h[2 * e], 0x07060302u);
-    mid[e] = __builtin_amdgcn_perm(m[2 * e + 1], m[2 * e], 0x07060302u);
-    lo[e] = __builtin_amdgcn_perm(l[2 * e + 1], l[2 * e], 0x07060302u);
-  }
-}
-
-__device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4_t& v) { return __builtin_bit_cast(bf16x8_t, v); }
+// (split_bf16x3, u32x4_t and as_bf16x8: common.h)
 
 constexpr int kBf3QK = 128;                     // K per quarter (LDS split stage)
 constexpr int kBf3Plane = kMlpRows * kBf3QK;    // bf16 elements per plane (row-major, 256 B rows)

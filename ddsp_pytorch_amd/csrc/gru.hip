@@ -172,13 +172,15 @@ __global__ void __launch_bounds__(kBS * kKC) gru_step_kernel(const float* __rest
 // The h_t addresses are fresh every step (the output sequence), so no cache holds an older copy.  Every
 // wait is bounded: a launch whose workgroups cannot all be resident at once sets an abort word and ends
 // (garbage out) instead of hanging.  The slot's 48 rows of W_hh (gates r, z, n of its 16 units) live in
-// REGISTERS for the whole sequence: lane l of wave w holds rows 6 (l >> 3) .. + 5 at k = 64 w + 8 (l & 7)
-// .. + 7 (48 values).  Per step h_{t-1} of the group's items is staged once into LDS (16 KB), each lane
-// reads its 8 k of all 8 items (384 FMAs), the 8 k octets of a row group are summed in a DPP half-row,
-// the 8 waves through LDS, and 128 epilogue threads apply the gates, one (item, unit) each.  (Per-step
-// phases by in-kernel stamps, tools/exp_gru_clock.py: W streamed from LDS and h loaded per lane from L2,
-// the lanes' operand traffic — 128-256 KB per CU per step through the 64 B/clk load path — cost 2.9-3.4
-// us of a 4.8-5.0 us step.)
+// REGISTERS for the whole sequence, split once into three bf16 terms (common.h split_bf16x3) as the A
+// fragments of v_mfma_f32_16x16x32_bf16: wave w owns k in [64 w, 64 w + 64) — two 32-wide chunks — and per
+// gate one 16 x 32 tile (rows = the slot's 16 units) per chunk.  Per step h_{t-1} of the group's items is
+// staged once into LDS (16 KB); each wave splits its 64 k of the 8 items into B fragments (items are the
+// tile's columns; columns 8-15 are zero) and runs 3 gates x 2 chunks x 6 products = 36 MFMAs — an
+// fp32-accurate W_hh h — the 8 waves' partial sums meet in LDS and 128 epilogue threads apply the gates, one
+// (item, unit) each.  (Per-step phases by in-kernel stamps, tools/exp_gru_clock.py: on the fp32 VALU — 384
+// FMAs per lane plus a DPP and an LDS reduction — the compute phase took 1.9 us of a 3.7-3.8 us step,
+// profiles/r06k_gruclk.log.)
 constexpr int kPG = 8;             // groups (items g, g + 8, ... belong to group g)
 constexpr int kPS = 32;            // slots per group
 constexpr int kPU = 16;            // hidden units per slot (hidden = kPS * kPU = 512)
@@ -221,14 +223,6 @@ __device__ __forceinline__ bool wait_at_least(uint32_t* word, uint32_t target, u
   return true;
 }
 
-// sum over the 8 lanes l & ~7 .. l | 7 (a DPP half-row), in every lane: VALU only
-__device__ __forceinline__ float dpp_sum8(float v) {
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
-  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
-  return v;
-}
-
 // An aborted launch (a workgroup that could not be resident within kPSpinTicks: beside another long-running
 // kernel, on a CU-masked stream, under GPU sharing) simply ends: every workgroup that sees the abort word
 // returns.  The outputs are then recomputed by gru_rescue_kernel, which the same call enqueues behind the
@@ -242,26 +236,23 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
                                                     float* __restrict__ h_last, float* __restrict__ save, int B, int T,
                                                     int g, int s, uint32_t* __restrict__ counter,
                                                     uint32_t* __restrict__ abort_word, __amdgpu_buffer_rsrc_t rout,
-                                                    float* hs, float (*part)[kPR][kPI], int* s_abort) {
+                                                    float* hs, float (*part)[kPI][kPR], int* s_abort) {
   constexpr int kStoreAux = kLocal ? 0 : 16;  // write-back into the XCD's L2, or write-through (sc1)
   const int nI = B > g ? (B - g + kPG - 1) / kPG : 0;  // items of this group
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  // lane -> 6 rows (row group rg of 8: rows 6 rg .. 6 rg + 5, row rho = gate * 16 + unit) x 8 k (k octet
-  // ks of the wave's 64); the 8 lanes of one row group are contiguous, so its k partials sum in a DPP half-row
-  const int ks = l & 7, rg = l >> 3;
-  const int kbase = 64 * w + 8 * ks;
+  const int q = l >> 4, l16 = l & 15;
   const int64_t item_stride = (int64_t)T * kPH;  // floats between items in out
   const int u0 = s * kPU;
-  // this lane's 48 weights of the slot's W_hh rows, in registers for the whole sequence
-  float wr[6][8];
+  // this lane's A fragments: gate gt, chunk c: W_hh[gt * 512 + u0 + l16][64 w + 32 c + 8 q .. + 7], split
+  u32x4_t wa[3][2][3];
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const int rho = 6 * rg + j, gate = rho / kPU, u = rho - gate * kPU;
-    const float* src = w_hh + (int64_t)(gate * kPH + u0 + u) * kPH + kbase;
-    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-    wr[j][0] = a.x; wr[j][1] = a.y; wr[j][2] = a.z; wr[j][3] = a.w;
-    wr[j][4] = b.x; wr[j][5] = b.y; wr[j][6] = b.z; wr[j][7] = b.w;
-  }
+  for (int gt = 0; gt < 3; ++gt)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float* src = w_hh + (int64_t)(gt * kPH + u0 + l16) * kPH + 64 * w + 32 * c + 8 * q;
+      split_bf16x3(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), wa[gt][c][0],
+                   wa[gt][c][1], wa[gt][c][2]);
+    }
   // epilogue role: e < 128 -> unit u0 + eu of item ei
   const int eu = tid & 15, ei = tid >> 4;
   const bool epi = tid < kPU * kPI && ei < nI;
@@ -307,44 +298,43 @@ __device__ __forceinline__ void gru_persistent_body(const float* __restrict__ xp
       *reinterpret_cast<float4*>(&hs[hi * kPH + hk + 4]) = b;
     }
     __syncthreads();
-    float acc[6][kPI];
+    // W_hh h_{t-1} for this wave's 64 k: item l16 (< 8; the other columns zero) is the tiles' column
+    f32x4_t acc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int i = 0; i < kPI; ++i) {
-      const float4 ha = *reinterpret_cast<const float4*>(&hs[i * kPH + kbase]);
-      const float4 hb4 = *reinterpret_cast<const float4*>(&hs[i * kPH + kbase + 4]);
+    for (int c = 0; c < 2; ++c) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (l16 < kPI) {
+        a = *reinterpret_cast<const float4*>(&hs[l16 * kPH + 64 * w + 32 * c + 8 * q]);
+        b = *reinterpret_cast<const float4*>(&hs[l16 * kPH + 64 * w + 32 * c + 8 * q + 4]);
+      }
+      u32x4_t hb[3];
+      split_bf16x3(a, b, hb[0], hb[1], hb[2]);
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        float v = wr[j][0] * ha.x;
-        v = fmaf(wr[j][1], ha.y, v);
-        v = fmaf(wr[j][2], ha.z, v);
-        v = fmaf(wr[j][3], ha.w, v);
-        v = fmaf(wr[j][4], hb4.x, v);
-        v = fmaf(wr[j][5], hb4.y, v);
-        v = fmaf(wr[j][6], hb4.z, v);
-        v = fmaf(wr[j][7], hb4.w, v);
-        acc[j][i] = v;
+      for (int gt = 0; gt < 3; ++gt) {  // small terms first
+        f32x4_t v = acc[gt];
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][1]), as_bf16x8(hb[1]), v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][2]), as_bf16x8(hb[0]), v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][0]), as_bf16x8(hb[2]), v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][1]), as_bf16x8(hb[0]), v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][0]), as_bf16x8(hb[1]), v, 0, 0, 0);
+        acc[gt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[gt][c][0]), as_bf16x8(hb[0]), v, 0, 0, 0);
       }
     }
+    // acc[gt][e]: unit 4 q + e, item l16 -> part[w][item][gt * 16 + unit]
+    if (l16 < kPI) {
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
-#pragma unroll
-      for (int i = 0; i < kPI; ++i) acc[j][i] = dpp_sum8(acc[j][i]);  // over the wave's 8 k octets
-    if (ks == 0) {
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int i = 0; i < kPI; i += 4)
-          *reinterpret_cast<float4*>(&part[w][6 * rg + j][i]) =
-              make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);
+      for (int gt = 0; gt < 3; ++gt)
+        *reinterpret_cast<float4*>(&part[w][l16][gt * kPU + 4 * q]) =
+            make_float4(acc[gt][0], acc[gt][1], acc[gt][2], acc[gt][3]);
     }
     __syncthreads();
     if (epi) {
       float hr = 0.f, hz = 0.f, hn = 0.f;
 #pragma unroll
       for (int v = 0; v < 8; ++v) {  // over the 8 waves, fixed order
-        hr += part[v][eu][ei];
-        hz += part[v][kPU + eu][ei];
-        hn += part[v][2 * kPU + eu][ei];
+        hr += part[v][ei][eu];
+        hz += part[v][ei][kPU + eu];
+        hn += part[v][ei][2 * kPU + eu];
       }
       const float r = sigmoidf_(exr + (hr + ebr));
       const float z = sigmoidf_(exz + (hz + ebz));
@@ -380,7 +370,7 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
     const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
     int B, int T, uint32_t* __restrict__ sync, int flags) {
   __shared__ __attribute__((aligned(16))) float hs[kPI * kPH];      // h_{t-1} of the group's items, 16 KB
-  __shared__ __attribute__((aligned(16))) float part[8][kPR][kPI];  // per-wave k partials
+  __shared__ __attribute__((aligned(16))) float part[8][kPI][kPR];  // per-wave k partials [wave][item][row]
   __shared__ int s_abort, s_local, s_slot, s_group;
   const int tid = threadIdx.x;
   uint32_t* abort_word = sync + kPAbortWord;
@@ -692,7 +682,6 @@ __global__ void __launch_bounds__(512) gru_bwd_step_mfma_kernel(
     float* __restrict__ dh_outbuf, int B, int T, int t) {
   constexpr int H = kH, K = 3 * H, kKW = K / 8, kCh = kKW / 16;
   static_assert(H % 128 == 0, "tile shape");
-  typedef float f32x4_t __attribute__((ext_vector_type(4)));
   __shared__ float part[8][16][17];  // [wave][batch row][unit]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int q = lane >> 4, l16 = lane & 15;

@@ -20,11 +20,13 @@ for _ in range(3):
     _lib.call("gru_forward_persistent", _lib.ptr(xp), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(out), None, None,
               B, T, H, 0, _lib.ptr(ws), ws.numel(), _lib.stream_of(out))
 torch.cuda.synchronize()
-st = ws.view(torch.int32)[18 * 32:18 * 32 + 8 * T].view(T, 8)[:, :5].cpu().long()
+st = ws.view(torch.int32)[17 * 32 + 64:17 * 32 + 64 + 8 * T].view(T, 8)[:, :6].cpu().long()
 st = (st - st[0, 0]) * 10  # ns
 d = st[1:, :] - st[:-1, :]
 ph = {"step_ns": float(d[10:, 0].float().median()), "wait_poll_ns": float((st[10:, 1] - st[10:, 0]).float().median()),
       "load_compute_ns": float((st[10:, 2] - st[10:, 1]).float().median()),
+      "stage_ns": float((st[10:, 5] - st[10:, 1]).float().median()),
+      "compute_ns": float((st[10:, 2] - st[10:, 5]).float().median()),
       "gates_store_ns": float((st[10:, 3] - st[10:, 2]).float().median()),
       "publish_ns": float((st[10:, 4] - st[10:, 3]).float().median()),
       "total_us": float(st[-1, 4]) / 1e3}

@@ -19,15 +19,17 @@ STEM = {"gru8": "gru", "gru16h2": "gru", "gru16h8": "gru", "gru32": "gru", "gruc
 # gruclk: per-step realtime stamps (100 MHz) of workgroup 0 of the persistent GRU, written after the
 # sync words (tools/exp_gru_clock.py reads them): 0 step start, 1 poll passed, 2 partials in LDS,
 # 3 gates stored, 4 counter added
-_STAMP = "if (blockIdx.x == 0 && tid == 0) abort_word[32 + 8 * t + {k}] = (uint32_t)__builtin_amdgcn_s_memrealtime();"
+_STAMP = "if (blockIdx.x == 0 && tid == 0) abort_word[64 + 8 * t + {k}] = (uint32_t)__builtin_amdgcn_s_memrealtime();"
 PROBES = {
-    "gruclk": [("constexpr int kPSyncWords = 18 * kPCounterStride;", "constexpr int kPSyncWords = 18 * kPCounterStride + 8 * 8192;"),
+    "gruclk": [("constexpr int kPSyncWords = 19 * kPCounterStride;", "constexpr int kPSyncWords = 19 * kPCounterStride + 32 + 8 * 8192;"),
                ("    // the epilogue's input projection for this step: issued before the wait\n",
                 "    " + _STAMP.format(k=0) + "\n"),
-               ("      if (*s_abort) return;\n    }\n", "      if (*s_abort) return;\n    }\n    " + _STAMP.format(k=1) + "\n"),
+               ("      if (*s_abort) return;  // gru_rescue_kernel recomputes the outputs\n    }\n",
+                "      if (*s_abort) return;\n    }\n    " + _STAMP.format(k=1) + "\n"),
                ("make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);\n    }\n    __syncthreads();\n",
                 "make_float4(acc[j][i], acc[j][i + 1], acc[j][i + 2], acc[j][i + 3]);\n    }\n    __syncthreads();\n    " + _STAMP.format(k=2) + "\n"),
                ("      ehp = hnew;\n    }\n", "      ehp = hnew;\n    }\n    " + _STAMP.format(k=3) + "\n"),
+               ("    __syncthreads();\n    float acc[6][kPI];\n", "    __syncthreads();\n    " + _STAMP.format(k=5) + "\n    float acc[6][kPI];\n"),
                ("      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n",
                 "      if (tid == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n      " + _STAMP.format(k=4) + "\n")],
     # wgclk: per-workgroup start / end realtime stamps (100 MHz) and hardware ids of the fused synthesis
