@@ -78,6 +78,7 @@ SIGNATURES = {
     "ddsp_hip_dense_rows": (_I, [_P, _I, _I64, _P]),
     "ddsp_hip_mlp_block": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _F, _F, _P, _I64, _I64, _I64, _I,
                                 _P]),
+    "ddsp_hip_linear": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_layer_norm_leaky_relu": (_I, [_P, _I64, _P, _P, _P, _P, _F, _F, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_stack_rows": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _P]),
     "ddsp_hip_gru_forward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),

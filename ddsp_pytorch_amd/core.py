@@ -592,7 +592,7 @@ def gru_layer_launch(x, w_ih, b_ih, w_hh, b_hh, h0c, out, h_last, gates, persist
     ``gru_last_route`` tells which one ran.  Returns the route taken ("persistent" or "steps")."""
     B, T, I = x.shape
     H = w_hh.shape[1]
-    xp = torch.addmm(b_ih, _c(x).reshape(B * T, I), w_ih.t()).view(B, T, 3 * H)
+    xp = linear(_c(x).reshape(B * T, I), w_ih, b_ih).view(B, T, 3 * H)
     args = (_lib.ptr(xp), _lib.ptr(_c(w_hh)), _lib.ptr(_c(b_hh)), _lib.ptr(h0c), _lib.ptr(out), _lib.ptr(h_last),
             _lib.ptr(gates), B, T, H)
     # hidden 512, batch <= 64: the whole recurrence as one persistent launch (W_hh resident in registers, h
@@ -624,6 +624,20 @@ def gru_last_route(device=None):
         if not info["rescued"]:
             info["hand_off"] = "xcd_local" if word & GRU_STATUS_LOCAL else "write_through"
     return info
+
+
+def linear(x, weight, bias):
+    """x [rows, in] @ weight[out, in]^T + bias -> [rows, out] (no autograd): ddsp_hip_linear — the bf16 matrix
+    cores with the fp32-accurate three-term split — where it applies (in 512 / 1024, out a multiple of 512),
+    else torch.addmm (hipBLASLt)."""
+    _dev(x, weight, bias)
+    rows, K = x.shape
+    N = weight.shape[0]
+    xc, wc, bc = _c(x), _c(weight), _c(bias)
+    y = torch.empty(rows, N, dtype=torch.float32, device=x.device)
+    st = _lib.call("linear", _lib.ptr(xc), K, K, _lib.ptr(wc), K, _lib.ptr(bc), _lib.ptr(y), N, rows, N,
+                   _lib.stream_of(y), allow=(ERANGE,))
+    return torch.addmm(bias, x, weight.t()) if st == ERANGE else y
 
 
 MLP_EXACT_F32 = 1  # include/ddsp_hip.h DDSP_HIP_MLP_EXACT_F32

@@ -536,13 +536,16 @@ __global__ void __launch_bounds__(512) mlp_block_res_kernel(
 constexpr int kBf3QK = 128;                     // K per quarter (LDS split stage)
 constexpr int kBf3Plane = kMlpRows * kBf3QK;    // bf16 elements per plane (row-major, 256 B rows)
 
-template <int kP>
-__global__ void __launch_bounds__(512) mlp_block_bf3_kernel(
+// kLN: the MLP block (512 outputs, LayerNorm + LeakyReLU epilogue); else a plain Linear, y = x W^T + b, over
+// 512-column blocks of W (blockIdx.y), e.g. the GRU's input projection for every step (decoder.py:41).
+template <int kP, int K, bool kLN>
+__global__ void __launch_bounds__(512) linear_bf3_kernel(
     const float* __restrict__ x, int64_t x_ld, const float* __restrict__ w, int64_t w_ld,
     const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float slope, float* __restrict__ y,
     int64_t y_ld, int64_t R) {
-  constexpr int K = kMlpResK, NQ = K / kBf3QK, NC = kBf3QK / 32;  // quarters; 32-wide chunks per quarter
+  constexpr int NQ = K / kBf3QK, NC = kBf3QK / 32;  // quarters; 32-wide chunks per quarter
+  static_assert(K % kBf3QK == 0 && NQ >= 2, "K");
   static_assert((NQ * NC) % kP == 0 && NC % kP == 0, "ring");
   // [buffer][plane hi/mid/lo][row][128 k] bf16, quads (8 bf16) at position Q ^ (row & 15)
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * 3 * kBf3Plane / 2];
@@ -551,6 +554,11 @@ __global__ void __launch_bounds__(512) mlp_block_bf3_kernel(
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int q = lane >> 4, l16 = lane & 15;
   const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
+  if (!kLN) {  // this workgroup's 512 output columns
+    w += (int64_t)blockIdx.y * kMlpN * w_ld;
+    bias += blockIdx.y * kMlpN;
+    y += blockIdx.y * kMlpN;
+  }
   // W fragment of this lane: column 64 wv + 16 j + l16, k = 32 h + 8 q .. + 7 (two float4)
   const float* wl = w + (int64_t)(64 * wv + l16) * w_ld + 8 * q;
   const int64_t wj = 16 * w_ld;
@@ -642,7 +650,22 @@ __global__ void __launch_bounds__(512) mlp_block_bf3_kernel(
       }
     }
   }
-  mlp_epilogue(acc, r0, K, w, w_ld, bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, R, red, stat);
+  if constexpr (kLN) {
+    mlp_epilogue(acc, r0, K, w, w_ld, bias, e0, e1, e_ld, gamma, beta, eps, slope, y, y_ld, R, red, stat);
+  } else {  // acc[i][j][e]: row 16 i + 4 q + e, column 64 wv + 16 j + l16
+    float cb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cb[j] = bias[64 * wv + 16 * j + l16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = r0 + 16 * i + 4 * q + e;
+        if (row >= R) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[row * y_ld + 64 * wv + 16 * j + l16] = acc[i][j][e] + cb[j];
+      }
+  }
 }
 
 // The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
@@ -734,7 +757,7 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (in_features == kMlpResK && vec == 4 && (flags & DDSP_HIP_MLP_EXACT_F32) == 0)  // the decoder's blocks
-    hipLaunchKernelGGL(mlp_block_bf3_kernel<2>, grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
+    hipLaunchKernelGGL((linear_bf3_kernel<2, kMlpResK, true>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
                        beta, eps, slope, y, y_ld, rows);
   else if (in_features == kMlpResK && vec == 4)  // x resident, W streamed to registers, f32 MFMA
     hipLaunchKernelGGL(mlp_block_res_kernel<4>, grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
@@ -748,6 +771,26 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
   else
     hipLaunchKernelGGL(mlp_block_kernel<1>, grid, dim3(512), 0, st, x, x_ld, (int)in_features, w, w_ld, bias, e0, e1,
                        e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  return launch_status();
+}
+
+int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
+                    const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1 || !w || !bias) return DDSP_HIP_EINVAL;
+  if (rows == 0) return DDSP_HIP_OK;
+  if (!x || !y || x_ld < in_features || w_ld < in_features || y_ld < out_features) return DDSP_HIP_EINVAL;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
+  if ((in_features != 512 && in_features != 1024) || out_features % kMlpN || (al & 15) || (x_ld & 3) || (w_ld & 3) ||
+      (rows + kMlpRows - 1) / kMlpRows > INT32_MAX || out_features / kMlpN > 65535)
+    return DDSP_HIP_ERANGE;  // callers keep their library GEMM
+  const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows), (unsigned)(out_features / kMlpN));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (in_features == 1024)
+    hipLaunchKernelGGL((linear_bf3_kernel<2, 1024, false>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, nullptr,
+                       nullptr, 0, nullptr, nullptr, 0.0f, 0.0f, y, y_ld, rows);
+  else
+    hipLaunchKernelGGL((linear_bf3_kernel<2, 512, false>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, nullptr,
+                       nullptr, 0, nullptr, nullptr, 0.0f, 0.0f, y, y_ld, rows);
   return launch_status();
 }
 

@@ -283,6 +283,14 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);
 
+/* A Linear y = x W^T + b (W [out_features, w_ld], the nn.Linear / nn.GRU weight layout) on the bf16 matrix cores
+ * with the fp32-accurate three-term split of ddsp_hip_mlp_block: the decoder's GRU input projection for every
+ * step at once (decoder.py:41, torch.nn.GRU's x W_ih^T + b_ih; 12,800 x 1024 -> 1536 at config 2).
+ * in_features 512 or 1024, out_features a multiple of 512, x and W 16-byte aligned with ld % 4 == 0; else
+ * DDSP_HIP_ERANGE (callers keep their library GEMM). */
+int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
+                    const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream);
+
 /* decoder.py:106-117 (param = harmonic_proj(hidden), magnitudes = noise_proj(hidden)): the two projections'
  * parameters stacked into one zero-padded matrix w [n_pad, in_features] and
  * bias b [n_pad] (caller buffers; rows n1 + n2 .. n_pad - 1 zero), for one library GEMM over both at a

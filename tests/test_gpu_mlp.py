@@ -182,3 +182,21 @@ def test_mlp_block_bf16x3_is_fp32_accurate(dd):
     e32, e3 = (f32.double() - ref), (bf3.double() - ref)
     rms = lambda e: float(e.pow(2).mean().sqrt())
     assert rms(e3) < 2 * rms(e32) and float(e3.abs().max()) < 2 * float(e32.abs().max()), (rms(e3), rms(e32))
+
+
+@pytest.mark.parametrize("rows,K,N", [(12800, 1024, 1536), (100, 512, 512), (65, 1024, 512), (7, 96, 512)])
+def test_linear_bf16x3(dd, rows, K, N):
+    """core.linear (ddsp_hip_linear: the GRU's input projection for every step, decoder.py:41) against an fp64
+    evaluation: within 2x of the f32 GEMM's (torch.addmm) error; K = 96 is outside the kernel and runs addmm."""
+    torch.manual_seed(rows + K)
+    x = torch.randn(rows, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") / K ** 0.5
+    b = torch.randn(N, device="cuda")
+    with torch.no_grad():
+        y = dd.core.linear(x, w, b)
+        y32 = torch.addmm(b, x, w.t())
+        ref = torch.addmm(b.double(), x.double(), w.double().t())
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    assert y.shape == (rows, N)
+    assert rms(y.double() - ref) <= 2 * rms(y32.double() - ref) + 1e-12, (rms(y.double() - ref), rms(y32.double() - ref))
+    assert float((y.double() - ref).abs().max()) <= 2 * float((y32.double() - ref).abs().max()) + 1e-12

@@ -40,3 +40,21 @@ flop = 2.0 * rows * 512 * 512
 res["tflops_resident"] = round(flop / (res["resident_us"] * 1e-6) / 1e12, 1)
 res["tflops_bf16x3"] = round(flop / (res["bf16x3_us"] * 1e-6) / 1e12, 1)
 print(json.dumps(res))
+
+# the GRU input projection: 12,800 x 1024 -> 1536 (decoder.py:41) on ddsp_hip_linear vs torch.addmm
+xg = torch.randn(rows, 1024, device="cuda")
+wg = torch.randn(1536, 1024, device="cuda") * 0.03
+bg = torch.randn(1536, device="cuda")
+res2 = {}
+for name, fn in (("linear_bf16x3", lambda: dd.core.linear(xg, wg, bg)), ("addmm", lambda: torch.addmm(bg, xg, wg.t())),
+                 ("linear_bf16x3_2", lambda: dd.core.linear(xg, wg, bg)), ("addmm_2", lambda: torch.addmm(bg, xg, wg.t()))):
+    for _ in range(10):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    res2[name + "_us"] = round(e0.elapsed_time(e1) / 20 * 1e3, 2)
+print(json.dumps(res2))
