@@ -538,7 +538,8 @@ constexpr int kBf3Plane = kMlpRows * kBf3QK;    // bf16 elements per plane (row-
 
 // kLN: the MLP block (512 outputs, LayerNorm + LeakyReLU epilogue); else a plain Linear, y = x W^T + b, over
 // 512-column blocks of W (blockIdx.y), e.g. the GRU's input projection for every step (decoder.py:41).
-template <int kP, int K, bool kLN>
+// kW8: W rows only 8-byte aligned (the out_mlp's first Linear, 514 inputs: decoder.py:68) -> 8-byte loads.
+template <int kP, int K, bool kLN, bool kW8 = false>
 __global__ void __launch_bounds__(512) linear_bf3_kernel(
     const float* __restrict__ x, int64_t x_ld, const float* __restrict__ w, int64_t w_ld,
     const float* __restrict__ bias, const float* __restrict__ e0, const float* __restrict__ e1, int64_t e_ld,
@@ -562,13 +563,21 @@ __global__ void __launch_bounds__(512) linear_bf3_kernel(
   // W fragment of this lane: column 64 wv + 16 j + l16, k = 32 h + 8 q .. + 7 (two float4)
   const float* wl = w + (int64_t)(64 * wv + l16) * w_ld + 8 * q;
   const int64_t wj = 16 * w_ld;
+  auto ldw = [](const float* p) -> float4 {
+    if constexpr (kW8) {
+      const float2 a = *reinterpret_cast<const float2*>(p), b = *reinterpret_cast<const float2*>(p + 2);
+      return make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      return *reinterpret_cast<const float4*>(p);
+    }
+  };
   float4 wb[kP][4][2];
 #pragma unroll
   for (int p = 0; p < kP; ++p)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      wb[p][j][0] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * p);
-      wb[p][j][1] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * p + 4);
+      wb[p][j][0] = ldw(wl + j * wj + 32 * p);
+      wb[p][j][1] = ldw(wl + j * wj + 32 * p + 4);
     }
   // split role: thread -> row t >> 3, k 16 (t & 7) .. + 15 of a quarter (quads Q = 2 (t & 7), + 1)
   const int srow = t >> 3, sq = 2 * (t & 7);
@@ -636,8 +645,8 @@ __global__ void __launch_bounds__(512) linear_bf3_kernel(
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          wb[p][j][0] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * hn);
-          wb[p][j][1] = *reinterpret_cast<const float4*>(wl + j * wj + 32 * hn + 4);
+          wb[p][j][0] = ldw(wl + j * wj + 32 * hn);
+          wb[p][j][1] = ldw(wl + j * wj + 32 * hn + 4);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the refill here (the scheduler would sink it to its use)
       }
@@ -756,9 +765,14 @@ int ddsp_hip_mlp_block(const float* x, int64_t x_ld, int64_t in_features, const 
                                       : (x_ld % 2 == 0 && w_ld % 2 == 0 && (al & 7) == 0) ? 2 : 1;
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (in_features == kMlpResK && vec == 4 && (flags & DDSP_HIP_MLP_EXACT_F32) == 0)  // the decoder's blocks
-    hipLaunchKernelGGL((linear_bf3_kernel<2, kMlpResK, true>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
-                       beta, eps, slope, y, y_ld, rows);
+  const bool x16 = x_ld % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (in_features == kMlpResK && x16 && (flags & DDSP_HIP_MLP_EXACT_F32) == 0 && vec == 4)  // the decoder's blocks
+    hipLaunchKernelGGL((linear_bf3_kernel<2, kMlpResK, true>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1,
+                       e_ld, gamma, beta, eps, slope, y, y_ld, rows);
+  else if (in_features == kMlpResK && x16 && (flags & DDSP_HIP_MLP_EXACT_F32) == 0 && w_ld % 2 == 0 &&
+           (reinterpret_cast<uintptr_t>(w) & 7) == 0)  // W rows 8-byte aligned: the out_mlp's first block
+    hipLaunchKernelGGL((linear_bf3_kernel<2, kMlpResK, true, true>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0,
+                       e1, e_ld, gamma, beta, eps, slope, y, y_ld, rows);
   else if (in_features == kMlpResK && vec == 4)  // x resident, W streamed to registers, f32 MFMA
     hipLaunchKernelGGL(mlp_block_res_kernel<4>, grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, e0, e1, e_ld, gamma,
                        beta, eps, slope, y, y_ld, rows);

@@ -11,12 +11,30 @@ inside ``FilteredNoise.forward`` (modules.py:119-123).  ``noise_mode = "torch"``
 reference sample for sample; ``"device"`` draws U[-1,1) with Philox4x32-10 inside the
 kernel (throughput mode: no host RNG, no H2D copy, no HBM read of noise).
 """
+import weakref
+
 import torch
 import torch.nn as nn
 
 from . import core, grad
 
 NOISE_MODES = ("torch", "device")
+
+
+# the stream that last used each reverb IR cache (Reverb._ir_cache), by id of the cache tensor with a weak
+# reference to it (a recycled id is not mistaken for the cache); entries go with their cache
+_CACHE_STREAM = {}
+
+
+def _cache_last_stream(c):
+    e = _CACHE_STREAM.get(id(c))
+    return e[1] if e is not None and e[0]() is c else None
+
+
+def _cache_set_stream(c, stream):
+    if id(c) not in _CACHE_STREAM or _CACHE_STREAM[id(c)][0]() is not c:
+        weakref.finalize(c, _CACHE_STREAM.pop, id(c), None)
+    _CACHE_STREAM[id(c)] = (weakref.ref(c), stream)
 
 
 class Reverb(nn.Module):
@@ -57,16 +75,18 @@ class Reverb(nn.Module):
         the common case, costs nothing."""
         caches = self.__dict__.setdefault("_ir_caches", {})
         key = (self.noise.device, int(n_samples), int(self.length))
-        entry = caches.get(key)
-        if entry is None:
+        c = caches.get(key)
+        if c is None:
             c = torch.zeros(core.reverb_cache_bytes(n_samples, self.length), dtype=torch.uint8,
                             device=self.noise.device)
-            entry = caches[key] = [c, torch.cuda.current_stream(c.device)]
-        cur = torch.cuda.current_stream(entry[0].device)
-        if cur != entry[1]:
-            cur.wait_stream(entry[1])
-            entry[1] = cur
-        return entry[0]
+            caches[key] = c
+        cur = torch.cuda.current_stream(c.device)
+        last = _cache_last_stream(c)  # kept outside the module: streams are not copyable (deepcopy, pickling)
+        if last is not None and last != cur:
+            cur.wait_stream(last)
+        if last != cur:
+            _cache_set_stream(c, cur)
+        return c
 
     def _forward_cached(self, x):
         """-> (out, workspace, spectrum): the reverb with the validated device cache (one launch group)."""
