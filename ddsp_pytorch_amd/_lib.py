@@ -85,6 +85,7 @@ SIGNATURES = {
     "ddsp_hip_gru_persistent_workspace_size": (_SZ, []),
     "ddsp_hip_gru_persistent_status_offset": (_SZ, []),
     "ddsp_hip_gru_forward_persistent": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I, _P, _SZ, _P]),
+    "ddsp_hip_gru_backward_persistent": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I, _P, _SZ, _P]),
     "ddsp_hip_gru_backward_workspace_size": (_SZ, [_I64, _I64]),
     "ddsp_hip_gru_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _SZ, _P]),
     # multiscale STFT (training loss)

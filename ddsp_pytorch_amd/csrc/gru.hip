@@ -365,17 +365,12 @@ __global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* __restrict__ 
   for (int i = threadIdx.x; i < n; i += 256) w[i] = 0u;
 }
 
-__global__ void __launch_bounds__(512) gru_persistent_kernel(
-    const float* __restrict__ xp, const float* __restrict__ w_hh, const float* __restrict__ b_hh,
-    const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
-    int B, int T, uint32_t* __restrict__ sync, int flags) {
-  __shared__ __attribute__((aligned(16))) float hs[kPI * kPH];      // h_{t-1} of the group's items, 16 KB
-  __shared__ __attribute__((aligned(16))) float part[8][kPI][kPR];  // per-wave k partials [wave][item][row]
-  __shared__ int s_abort, s_local, s_slot, s_group;
-  const int tid = threadIdx.x;
+// The persistent launches' start (forward and BPTT): this workgroup's XCD and its ticket there, then every
+// workgroup's arrival (bounded: an abort, never a hang); the group / slot assignment and the hand-off form.
+__device__ void persistent_census(uint32_t* __restrict__ sync, int flags, int* s_abort, int* s_local, int* s_group,
+                                  int* s_slot) {
   uint32_t* abort_word = sync + kPAbortWord;
-  // census: this workgroup's XCD and its ticket there, then every workgroup's arrival
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     xcc &= 7;
@@ -398,11 +393,23 @@ __global__ void __launch_bounds__(512) gru_persistent_kernel(
         __hip_atomic_store(sync + kPStatusWord, local ? (uint32_t)DDSP_HIP_GRU_STATUS_LOCAL : 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_abort = !ok;
-    s_local = local;
-    s_group = local ? (int)xcc : (int)(blockIdx.x % kPG);
-    s_slot = local ? (int)ticket : (int)(blockIdx.x / kPG);
+    *s_abort = !ok;
+    *s_local = local;
+    *s_group = local ? (int)xcc : (int)(blockIdx.x % kPG);
+    *s_slot = local ? (int)ticket : (int)(blockIdx.x / kPG);
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(512) gru_persistent_kernel(
+    const float* __restrict__ xp, const float* __restrict__ w_hh, const float* __restrict__ b_hh,
+    const float* __restrict__ h0, float* __restrict__ out, float* __restrict__ h_last, float* __restrict__ save,
+    int B, int T, uint32_t* __restrict__ sync, int flags) {
+  __shared__ __attribute__((aligned(16))) float hs[kPI * kPH];      // h_{t-1} of the group's items, 16 KB
+  __shared__ __attribute__((aligned(16))) float part[8][kPI][kPR];  // per-wave k partials [wave][item][row]
+  __shared__ int s_abort, s_local, s_slot, s_group;
+  uint32_t* abort_word = sync + kPAbortWord;
+  persistent_census(sync, flags, &s_abort, &s_local, &s_group, &s_slot);
   __syncthreads();
   if (s_abort) return;  // gru_rescue_kernel recomputes the outputs
   const int g = s_group, s = s_slot;
@@ -730,6 +737,219 @@ __global__ void __launch_bounds__(512) gru_bwd_step_mfma_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The BPTT as ONE persistent launch (hidden 512, batch <= 64; the training forward's mirror): the per-step
+// backward launches above pay a kernel boundary and re-stage W_hh every step (9.7 us per step at config 2,
+// 1.9 ms per layer).  Same groups, slots, census, hand-off and abort as the forward: slot s owns units
+// [16 s, 16 s + 16) of its group's 8 items and keeps its W_hh columns — the A fragments of W_hh^T (rows =
+// its 16 units, k = the 1536 gate rows; wave w owns k in [192 w, 192 w + 192), six 32-wide chunks), split
+// into three bf16 terms — in registers.  Per step t (T-1 down to 0): wait until every slot has published
+// dG_t = (da_r, da_z, dan r) — the grad_xp / grad_gn rows of step t themselves —, stage the group's 8 x 1536
+// values into LDS (48 KB), W_hh^T dG_t for the slot's units on the bf16 matrix cores (36 MFMAs per wave,
+// fp32-accurate), the 8 waves' partials through LDS, then 128 epilogue threads (unit, item):
+// dh_{t-1} = dh_t z_t + W_hh^T dG_t + dout_{t-1} and step t-1's elementwise part (its dG, written and
+// published); at t = 0 the last sums give dh0.  An abort (residency) leaves the outputs to
+// gru_bwd_rescue_kernel, enqueued behind it.
+__global__ void __launch_bounds__(512) gru_bptt_persistent_kernel(
+    const float* __restrict__ w_hh, const float* __restrict__ save, const float* __restrict__ out,
+    const float* __restrict__ h0, const float* __restrict__ dout, const float* __restrict__ dh_last,
+    float* __restrict__ dxp, float* __restrict__ dgn, float* __restrict__ dh0, int B, int T,
+    uint32_t* __restrict__ sync, int flags) {
+  constexpr int K3 = 3 * kPH;  // 1536 gate rows
+  __shared__ __attribute__((aligned(16))) float gs[kPI * K3];        // dG_t of the group's items, 48 KB
+  __shared__ __attribute__((aligned(16))) float part[8][kPI][kPU];   // per-wave partials [wave][item][unit]
+  __shared__ int s_abort, s_local, s_slot, s_group;
+  uint32_t* abort_word = sync + kPAbortWord;
+  persistent_census(sync, flags, &s_abort, &s_local, &s_group, &s_slot);
+  if (s_abort) return;  // gru_bwd_rescue_kernel recomputes the outputs
+  const int g = s_group, s = s_slot;
+  if (B <= g) return;
+  const bool local = s_local;
+  uint32_t* counter = sync + g * kPCounterStride;
+  const int nI = (B - g + kPG - 1) / kPG;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int q = l >> 4, l16 = l & 15;
+  const int u0 = s * kPU;
+  const int64_t plane = (int64_t)B * T * kPH;
+  // dxp / dgn as buffer resources (byte offsets < 2^31, checked by the host): the hand-off stores
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(dxp, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(dgn, (short)0, 0x7fffffff, 0x00020000);
+  // A fragments: chunk c, lane (q, l16): W_hh[192 w + 32 c + 8 q + j][u0 + l16], j = 0..7, split
+  u32x4_t wa[6][3];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    const float* src = w_hh + (int64_t)(192 * w + 32 * c + 8 * q) * kPH + u0 + l16;
+    const float4 a = make_float4(src[0], src[kPH], src[2 * kPH], src[3 * kPH]);
+    const float4 b = make_float4(src[4 * kPH], src[5 * kPH], src[6 * kPH], src[7 * kPH]);
+    split_bf16x3(a, b, wa[c][0], wa[c][1], wa[c][2]);
+  }
+  // epilogue role: tid < 128 -> unit u0 + eu of item ei
+  const int eu = tid & 15, ei = tid >> 4;
+  const bool epi = tid < kPU * kPI && ei < nI;
+  const int eb = g + kPG * ei;
+  const int j = u0 + eu;
+  // the elementwise part of step t for this (item, unit) from its saved gates and h_{t-1} (loaded ahead by
+  // load_elem): dG_t into dxp / dgn (write-back stores into the XCD's L2 on the local hand-off,
+  // write-through otherwise)
+  struct Elem { float r, z, n, hn, hprev, dout; };
+  auto load_elem = [&](int t) -> Elem {
+    const int64_t idx = ((int64_t)eb * T + t) * kPH + j;
+    Elem e;
+    e.r = save[idx];
+    e.z = save[plane + idx];
+    e.n = save[2 * plane + idx];
+    e.hn = save[3 * plane + idx];
+    e.hprev = t >= 1 ? out[idx - kPH] : (h0 ? h0[(int64_t)eb * kPH + j] : 0.0f);
+    e.dout = dout ? dout[idx] : 0.0f;
+    return e;
+  };
+  auto elem = [&](int t, float dh, const Elem& ev) {
+    const int64_t idx = ((int64_t)eb * T + t) * kPH + j;
+    const float r = ev.r, z = ev.z, n = ev.n, hn = ev.hn, hprev = ev.hprev;
+    const float dn = dh * (1.0f - z);
+    const float dz = dh * (hprev - n);
+    const float dan = dn * (1.0f - n * n);
+    const float daz = dz * z * (1.0f - z);
+    const float dar = dan * hn * r * (1.0f - r);
+    const int xo = (int)((((int64_t)eb * T + t) * 3 * kPH + j) * 4);
+    const int go = (int)(idx * 4);
+    if (local) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dar), rx, xo, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(daz), rx, xo + 4 * kPH, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dan), rx, xo + 8 * kPH, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dan * r), rg, go, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dar), rx, xo, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(daz), rx, xo + 4 * kPH, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dan), rx, xo + 8 * kPH, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(dan * r), rg, go, 0, 16);
+    }
+  };
+  float dh = 0.0f, zt = 0.0f;
+  if (epi) {  // step T-1: dh = dout_{T-1} + dh_last
+    const Elem ev = load_elem(T - 1);
+    dh = ev.dout + (dh_last ? dh_last[(int64_t)eb * kPH + j] : 0.0f);
+    zt = ev.z;
+    elem(T - 1, dh, ev);
+  }
+  // staging role: thread -> item tid >> 6, 24 floats (6 float4) at 24 (tid & 63) .. of its 1536
+  const int si = tid >> 6, sk = 24 * (tid & 63);
+  const bool sok = si < nI;
+  const int sb = g + kPG * (sok ? si : 0);
+  for (int t = T - 1; t >= 0; --t) {
+    // publish dG_t (written by this workgroup's epilogue threads): drained stores, barrier, one add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!wait_at_least(counter, (uint32_t)kPS * (uint32_t)(T - t), abort_word)) s_abort = 1;
+    }
+    Elem ev{};  // step t-1's elementwise operands: issued before the wait completes
+    if (epi && t >= 1) ev = load_elem(t - 1);
+    __syncthreads();
+    if (s_abort) return;
+    // dG_t of the group's items into LDS (zeros past nI)
+#pragma unroll
+    for (int v = 0; v < 6; ++v) {
+      const int k = sk + 4 * v;  // 4 consecutive gate rows, never crossing the 512-row gate planes
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sok) {
+        if (k < 2 * kPH) a = ld_sc1_f4(rx, (int)((((int64_t)sb * T + t) * 3 * kPH + k) * 4));
+        else a = ld_sc1_f4(rg, (int)((((int64_t)sb * T + t) * kPH + (k - 2 * kPH)) * 4));
+      }
+      *reinterpret_cast<float4*>(&gs[si * K3 + k]) = a;
+    }
+    __syncthreads();
+    // W_hh^T dG_t: units (rows) x items (columns 0..7; 8..15 zero)
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (l16 < kPI) {
+        a = *reinterpret_cast<const float4*>(&gs[l16 * K3 + 192 * w + 32 * c + 8 * q]);
+        b = *reinterpret_cast<const float4*>(&gs[l16 * K3 + 192 * w + 32 * c + 8 * q + 4]);
+      }
+      u32x4_t gb[3];
+      split_bf16x3(a, b, gb[0], gb[1], gb[2]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][1]), as_bf16x8(gb[1]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][2]), as_bf16x8(gb[0]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][0]), as_bf16x8(gb[2]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][1]), as_bf16x8(gb[0]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][0]), as_bf16x8(gb[1]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wa[c][0]), as_bf16x8(gb[0]), acc, 0, 0, 0);
+    }
+    if (l16 < kPI)  // acc[e]: unit 4 q + e, item l16
+      *reinterpret_cast<float4*>(&part[w][l16][4 * q]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (epi) {
+      float sum = 0.0f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) sum += part[v][ei][eu];  // over the 8 waves, fixed order
+      const float dprev = dh * zt + sum;  // dh_{t-1} without dout_{t-1}
+      if (t >= 1) {
+        dh = dprev + ev.dout;
+        zt = ev.z;
+        elem(t - 1, dh, ev);
+      } else if (dh0) {
+        dh0[(int64_t)eb * kPH + j] = dprev;
+      }
+    }
+  }
+}
+
+// The BPTT launch's rescue (as gru_rescue_kernel for the forward): nothing unless the launch aborted; then
+// one workgroup per item redoes the whole BPTT, thread = unit, W_hh^T dG_t read from global memory row by
+// row (coalesced over the units) — slow, never wrong.  fp32 sums in gate-row order.
+__global__ void __launch_bounds__(512) gru_bwd_rescue_kernel(
+    const float* __restrict__ w_hh, const float* __restrict__ save, const float* __restrict__ out,
+    const float* __restrict__ h0, const float* __restrict__ dout, const float* __restrict__ dh_last,
+    float* __restrict__ dxp, float* __restrict__ dgn, float* __restrict__ dh0, int B, int T,
+    uint32_t* __restrict__ sync) {
+  if (__hip_atomic_load(sync + kPAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  constexpr int K3 = 3 * kPH;
+  __shared__ float gs[K3];  // dG_t of this item
+  const int b = blockIdx.x, j = threadIdx.x;
+  const int64_t plane = (int64_t)B * T * kPH;
+  auto elem = [&](int t, float dh) -> float {
+    const int64_t idx = ((int64_t)b * T + t) * kPH + j;
+    const float r = save[idx], z = save[plane + idx], n = save[2 * plane + idx], hn = save[3 * plane + idx];
+    const float hprev = t >= 1 ? out[idx - kPH] : (h0 ? h0[(int64_t)b * kPH + j] : 0.0f);
+    const float dn = dh * (1.0f - z);
+    const float dz = dh * (hprev - n);
+    const float dan = dn * (1.0f - n * n);
+    const float daz = dz * z * (1.0f - z);
+    const float dar = dan * hn * r * (1.0f - r);
+    const int64_t xi = ((int64_t)b * T + t) * 3 * kPH + j;
+    dxp[xi] = dar;
+    dxp[xi + kPH] = daz;
+    dxp[xi + 2 * kPH] = dan;
+    dgn[idx] = dan * r;
+    gs[j] = dar;
+    gs[kPH + j] = daz;
+    gs[2 * kPH + j] = dan * r;
+    return z;
+  };
+  float dh = (dout ? dout[((int64_t)b * T + (T - 1)) * kPH + j] : 0.0f) + (dh_last ? dh_last[(int64_t)b * kPH + j] : 0.0f);
+  float zt = elem(T - 1, dh);
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    float sum = 0.0f;
+    for (int r = 0; r < K3; ++r) sum = fmaf(w_hh[(int64_t)r * kPH + j], gs[r], sum);
+    __syncthreads();  // every read of gs done before step t-1's elementwise part rewrites it
+    const float dprev = dh * zt + sum;
+    if (t >= 1) {
+      dh = dprev + (dout ? dout[((int64_t)b * T + (t - 1)) * kPH + j] : 0.0f);
+      zt = elem(t - 1, dh);
+      __syncthreads();
+    } else if (dh0) {
+      dh0[(int64_t)b * kPH + j] = dprev;
+    }
+  }
+  if (b == 0 && j == 0)
+    __hip_atomic_store(sync + kPStatusWord, (uint32_t)DDSP_HIP_GRU_STATUS_RESCUED, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 }  // namespace ddsp
 
@@ -738,6 +958,16 @@ using namespace ddsp;
 extern "C" {
 
 }  // extern "C"
+
+// false when the stream's CU mask leaves out some of the device's cus CUs (a query failure counts as all)
+static bool stream_reaches_all_cus(hipStream_t st, int cus) {
+  uint32_t mask[32] = {0};
+  const int words = (cus + 31) / 32;
+  if (words > 32 || hipExtStreamGetCUMask(st, (uint32_t)words, mask) != hipSuccess) return true;
+  int on = 0;
+  for (int c = 0; c < cus; ++c) on += (mask[c >> 5] >> (c & 31)) & 1u;
+  return on >= cus;
+}
 
 template <int kBS, int kKC, int kH = 0>
 static int gru_backward_steps(const float* w_t, const float* gates, int64_t plane, const float* grad_out, const float* out,
@@ -816,15 +1046,7 @@ int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const fl
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // a stream whose kernels cannot reach every CU (hipExtStreamCreateWithCUMask, e.g. this library's
   // ddsp_hip_stream_create_cu_masked) cannot hold the grid: refuse up front rather than wait for the abort
-  if (!(flags & DDSP_HIP_GRU_NO_MASK_CHECK)) {
-    uint32_t mask[32] = {0};
-    const int words = (cus + 31) / 32;
-    if (words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, mask) == hipSuccess) {
-      int on = 0;
-      for (int c = 0; c < cus; ++c) on += (mask[c >> 5] >> (c & 31)) & 1u;
-      if (on < cus) return DDSP_HIP_ERANGE;
-    }
-  }
+  if (!(flags & DDSP_HIP_GRU_NO_MASK_CHECK) && !stream_reaches_all_cus(st, cus)) return DDSP_HIP_ERANGE;
   uint32_t* sync = reinterpret_cast<uint32_t*>(workspace);
   // the sync words are zeroed by a kernel of ours: a hipMemsetAsync captured into a HIP graph wrote
   // 0x5EE0B080 instead of 0 on every replay after the first (ROCm 7.2, tools/dbg_gru_graph.py)
@@ -849,6 +1071,37 @@ int ddsp_hip_gru_forward(const float* xp, const float* w_hh, const float* b_hh, 
   if (hidden % 128 == 0)
     return gru_forward_launch<16, 32>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
   return gru_forward_launch<32, 16>(xp, w_hh, b_hh, h0, out, h_last, gates, batch, steps, hidden, stream);
+}
+
+int ddsp_hip_gru_backward_persistent(const float* w_hh, const float* gates, const float* out, const float* h0,
+                                     const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
+                                     float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, int flags,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (flags & ~(DDSP_HIP_GRU_SPREAD | DDSP_HIP_GRU_NO_MASK_CHECK | DDSP_HIP_GRU_FORCE_ABORT)) return DDSP_HIP_EINVAL;
+  if (batch < 0 || steps < 0 || hidden < 1) return DDSP_HIP_EINVAL;
+  if (batch == 0 || steps == 0) return DDSP_HIP_OK;
+  if (!w_hh || !gates || !out || !grad_xp || !grad_gn) return DDSP_HIP_EINVAL;
+  if (hidden != kPH || batch > kPG * kPI || batch * steps * 3 * hidden * (int64_t)sizeof(float) >= ((int64_t)1 << 31) ||
+      steps > (int64_t)INT32_MAX / kPS)
+    return DDSP_HIP_ERANGE;
+  if (!workspace || workspace_bytes < ddsp_hip_gru_persistent_workspace_size()) return DDSP_HIP_EWORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(grad_xp) | reinterpret_cast<uintptr_t>(grad_gn)) & 15) return DDSP_HIP_ERANGE;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return DDSP_HIP_ELAUNCH;
+  if (cus < kPG * kPS) return DDSP_HIP_ERANGE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!(flags & DDSP_HIP_GRU_NO_MASK_CHECK) && !stream_reaches_all_cus(st, cus)) return DDSP_HIP_ERANGE;
+  uint32_t* sync = reinterpret_cast<uint32_t*>(workspace);
+  hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, sync, kPSyncWords);
+  if (int r = launch_status()) return r;
+  hipLaunchKernelGGL(gru_bptt_persistent_kernel, dim3(kPG * kPS), dim3(512), 0, st, w_hh, gates, out, h0, grad_out,
+                     grad_h_last, grad_xp, grad_gn, grad_h0, (int)batch, (int)steps, sync, flags);
+  if (int r = launch_status()) return r;
+  hipLaunchKernelGGL(gru_bwd_rescue_kernel, dim3((unsigned)batch), dim3(512), 0, st, w_hh, gates, out, h0, grad_out,
+                     grad_h_last, grad_xp, grad_gn, grad_h0, (int)batch, (int)steps, sync);
+  return launch_status();
 }
 
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden) {

@@ -429,6 +429,9 @@ class StftMagFn(_F):
 
 
 # ------------------------------------------------------------------------------------------
+GRU_BPTT_FLAGS = 0  # ddsp_hip_gru_backward_persistent's test hooks (core.GRU_*); 0 in use
+
+
 class GRUFn(_F):
     """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 step kernels
     (csrc/gru.hip); the input projection and the weight gradients are plain GEMMs."""
@@ -456,12 +459,19 @@ class GRUFn(_F):
         dxp = torch.empty(B, T, 3 * H, dtype=torch.float32, device=x.device)
         dgn = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
         dh0 = torch.empty(B, H, dtype=torch.float32, device=x.device) if ctx.has_h0 else None
-        ws = core._workspace(_lib.query("gru_backward_workspace_size", B, H), x.device)
         go = core._c(g_out) if g_out is not None else None
         gh = core._c(g_hlast.reshape(B, H)) if g_hlast is not None else None
-        _lib.call("gru_backward", _lib.ptr(core._c(w_hh)), _lib.ptr(gates), _lib.ptr(out), _lib.ptr(h0p), _lib.ptr(go),
-                  _lib.ptr(gh), _lib.ptr(dxp), _lib.ptr(dgn), _lib.ptr(dh0), B, T, H, _lib.ptr(ws), ws.numel(),
-                  _lib.stream_of(dxp))
+        args = (_lib.ptr(core._c(w_hh)), _lib.ptr(gates), _lib.ptr(out), _lib.ptr(h0p), _lib.ptr(go), _lib.ptr(gh),
+                _lib.ptr(dxp), _lib.ptr(dgn), _lib.ptr(dh0), B, T, H)
+        # hidden 512, batch <= 64: the whole BPTT as one persistent launch; otherwise (ERANGE) one launch per step
+        ws = core._workspace(_lib.query("gru_persistent_workspace_size"), x.device)
+        st = _lib.call("gru_backward_persistent", *args, int(GRU_BPTT_FLAGS), _lib.ptr(ws), ws.numel(),
+                       _lib.stream_of(dxp), allow=(core.ERANGE,))
+        dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+        core._GRU_LAST[dev] = ("persistent", ws) if st == 0 else ("steps", None)
+        if st == core.ERANGE:
+            ws = core._workspace(_lib.query("gru_backward_workspace_size", B, H), x.device)
+            _lib.call("gru_backward", *args, _lib.ptr(ws), ws.numel(), _lib.stream_of(dxp))
         dxp2 = dxp.view(B * T, 3 * H)
         dG = torch.cat([dxp[..., :2 * H], dgn], -1).view(B * T, 3 * H)
         hprev = torch.cat([(h0p.view(B, 1, H) if h0p is not None else torch.zeros(B, 1, H, device=x.device)),

@@ -340,6 +340,17 @@ size_t ddsp_hip_gru_persistent_status_offset(void);
 int ddsp_hip_gru_forward_persistent(const float* xp, const float* w_hh, const float* b_hh, const float* h0, float* out,
                                     float* h_last, float* gates, int64_t batch, int64_t steps, int64_t hidden,
                                     int flags, void* workspace, size_t workspace_bytes, void* stream);
+/* The BPTT as ONE persistent launch (the training mirror of ddsp_hip_gru_forward_persistent: same envelope —
+ * hidden 512, batch <= 64, grad_xp < 2 GiB, >= 256 CUs, a stream that may use every CU; else DDSP_HIP_ERANGE and
+ * the caller uses ddsp_hip_gru_backward —, same groups, census, hand-off, flags, abort, rescue and status word):
+ * each workgroup keeps its 16 units' W_hh columns in registers and the slots hand each step's gate gradients
+ * (the grad_xp / grad_gn rows themselves) to each other; W_hh^T dG on the bf16 matrix cores with the
+ * fp32-accurate three-term split.  Outputs as ddsp_hip_gru_backward (fp32-accurate, not the same bits).
+ * Workspace: ddsp_hip_gru_persistent_workspace_size() bytes. */
+int ddsp_hip_gru_backward_persistent(const float* w_hh, const float* gates, const float* out, const float* h0,
+                                     const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,
+                                     float* grad_h0, int64_t batch, int64_t steps, int64_t hidden, int flags,
+                                     void* workspace, size_t workspace_bytes, void* stream);
 size_t ddsp_hip_gru_backward_workspace_size(int64_t batch, int64_t hidden);
 int ddsp_hip_gru_backward(const float* w_hh, const float* gates, const float* out, const float* h0,
                           const float* grad_out, const float* grad_h_last, float* grad_xp, float* grad_gn,

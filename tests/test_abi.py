@@ -141,3 +141,7 @@ def test_training_entry_points_reject_bad_arguments_without_launching():
     assert lib.ddsp_hip_gru_forward_persistent(one, one, one, null, one, null, null, 1, 4, 512, 0, one, 4,
                                                null) == EWS
     assert lib.ddsp_hip_gru_persistent_status_offset() + 4 <= lib.ddsp_hip_gru_persistent_workspace_size()
+    assert lib.ddsp_hip_gru_backward_persistent(one, one, one, null, null, null, one, one, null, 1, 4, 512, 8, one,
+                                                4096, null) == EINVAL
+    assert lib.ddsp_hip_gru_backward_persistent(one, one, one, null, null, null, one, one, null, 65, 4, 512, 0, one,
+                                                4096, null) == ERANGE

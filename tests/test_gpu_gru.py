@@ -221,3 +221,76 @@ def test_gru_persistent_write_through_hand_off(dd):
     assert sb == {"route": "persistent", "hand_off": "write_through", "rescued": False}, sb
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert relerr(b[0], ref_out) < 1e-5 and relerr(b[1], ref_h) < 1e-5
+
+
+def _bptt_case(dd, B, T, with_h0, seed):
+    """torch.nn.GRU's CPU autograd vs core.gru on the GPU for out * w + h_T * wl: every gradient."""
+    torch.manual_seed(seed)
+    g = torch.nn.GRU(1024, 512, batch_first=True)
+    x = torch.randn(B, T, 1024)
+    h0 = torch.randn(1, B, 512) * 0.5 if with_h0 else None
+    w = torch.randn(B, T, 512)
+    wl = torch.randn(1, B, 512)
+    xc = x.clone().requires_grad_(True)
+    h0c = h0.clone().requires_grad_(True) if with_h0 else None
+    out, hl = g(xc, h0c) if with_h0 else g(xc)
+    ((out * w).sum() + (hl * wl).sum()).backward()
+    ref = {n: p.grad.clone() for n, p in g.named_parameters()}
+    gg = g.cuda()
+    for p in gg.parameters():
+        p.grad = None
+    xg = x.cuda().requires_grad_(True)
+    h0g = h0.cuda().requires_grad_(True) if with_h0 else None
+    og, hg = dd.core.gru(xg, gg, h0g)
+    ((og * w.cuda()).sum() + (hg * wl.cuda()).sum()).backward()
+    torch.cuda.synchronize()
+    errs = {"x": relerr(xg.grad, xc.grad)}
+    errs.update({n: relerr(p.grad, ref[n]) for n, p in gg.named_parameters()})
+    if with_h0:
+        errs["h0"] = relerr(h0g.grad, h0c.grad)
+    return errs
+
+
+@pytest.mark.parametrize("B,T,with_h0", [(64, 200, False), (9, 31, True), (1, 1, True), (3, 2, False)])
+def test_gru_bptt_persistent(dd, monkeypatch, B, T, with_h0):
+    """Hidden 512, batch <= 64: the BPTT is ONE persistent launch (ddsp_hip_gru_backward_persistent, W_hh^T dG
+    on the bf16 matrix cores), every gradient within 1e-5 relative of torch's CPU autograd."""
+    calls = []
+    real = dd._lib.call
+
+    def spy(name, *a, **k):
+        st = real(name, *a, **k)
+        calls.append((name, st))
+        return st
+    monkeypatch.setattr(dd._lib, "call", spy)
+    errs = _bptt_case(dd, B, T, with_h0, B + 3 * T)
+    assert [st for n, st in calls if n == "gru_backward_persistent"] == [0], calls
+    assert not any(n == "gru_backward" for n, _ in calls)
+    assert dd.core.gru_last_route()["hand_off"] == "xcd_local"
+    assert max(errs.values()) < 1e-5, errs
+
+
+@pytest.mark.parametrize("flags", ["FORCE_ABORT", "SPREAD"])
+def test_gru_bptt_persistent_abort_and_spread(dd, monkeypatch, flags):
+    """The BPTT launch's abort path (its rescue kernel redoes the BPTT per item) and its placement-independent
+    hand-off: the gradients stay within 1e-5 of torch's autograd either way, and the status word says which."""
+    from ddsp_pytorch_amd import grad as _grad
+    monkeypatch.setattr(_grad, "GRU_BPTT_FLAGS", getattr(dd.core, "GRU_" + flags))
+    errs = _bptt_case(dd, 20, 12, True, 77)
+    st = dd.core.gru_last_route()
+    if flags == "FORCE_ABORT":
+        assert st["rescued"], st
+    else:
+        assert st == {"route": "persistent", "hand_off": "write_through", "rescued": False}, st
+    assert max(errs.values()) < 1e-5, errs
+
+
+def test_gru_bptt_on_cu_masked_stream(dd):
+    """On a 64-CU masked stream the persistent BPTT is refused up front and the step kernels run."""
+    s = dd.core.cu_masked_stream(range(64))
+    with torch.cuda.stream(s):
+        errs = _bptt_case(dd, 8, 16, False, 5)
+        st = dd.core.gru_last_route()
+    s.synchronize()
+    assert st["route"] == "steps", st
+    assert max(errs.values()) < 1e-5, errs

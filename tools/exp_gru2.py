@@ -58,3 +58,22 @@ with torch.no_grad():
             "gru_forward_persistent", _lib.ptr(xb), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(ob), None, None,
             b, T, H, 0, _lib.ptr(ws), ws.numel(), st()))
 print(json.dumps(res), flush=True)
+
+# the BPTT (training): ddsp_hip_gru_backward_persistent vs the per-step backward launches, on saved gates
+gates = torch.empty(4, B, T, H, device="cuda")
+with torch.no_grad():
+    _lib.call("gru_forward", _lib.ptr(xp), _lib.ptr(w_hh), _lib.ptr(b_hh), None, _lib.ptr(out), None, _lib.ptr(gates),
+              B, T, H, _lib.stream_of(out))
+gout = torch.randn(B, T, H, device="cuda")
+dxp = torch.empty(B, T, 3 * H, device="cuda")
+dgn = torch.empty(B, T, H, device="cuda")
+wsb = torch.empty(_lib.query("gru_backward_workspace_size", B, H), dtype=torch.uint8, device="cuda")
+bargs = lambda: (_lib.ptr(w_hh), _lib.ptr(gates), _lib.ptr(out), None, _lib.ptr(gout), None, _lib.ptr(dxp),  # noqa: E731
+                 _lib.ptr(dgn), None, B, T, H)
+res2 = {"bptt_steps_ms": dev_ms(lambda: _lib.call("gru_backward", *bargs(), _lib.ptr(wsb), wsb.numel(),
+                                                    _lib.stream_of(out)))}
+ref = dxp.clone()
+res2["bptt_persistent_ms"] = dev_ms(lambda: _lib.call("gru_backward_persistent", *bargs(), 0, _lib.ptr(ws), ws.numel(),
+                                                        _lib.stream_of(out)))
+res2["bptt_rel_diff"] = float((dxp - ref).norm() / ref.norm())
+print(json.dumps(res2), flush=True)
