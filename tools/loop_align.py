@@ -85,6 +85,32 @@ def analyze(so, kern="synth_frame_kernelILb1ELb0ELb0ELb0EE"):
             "sines": sum(1 for x in body if x[2].startswith("v_sin_f32"))}
 
 
+def analyze_all(so, kern="synth_frame_kernelILb1ELb0ELb0ELb0EE"):
+    """every innermost sine loop of the kernel (a kernel may carry more than one copy of its loop, e.g. the
+    fused forward's before- and after-the-noise-phases copies), in address order; analyze()'s fields"""
+    ins = kernel_instructions(so, kern)
+    loops = []
+    for i, (addr, size, txt) in enumerate(ins):
+        m = re.match(r"s_cbranch_\w+\s+(-?\d+)", txt)
+        if not m:
+            continue
+        off = int(m.group(1))
+        target = addr + 4 + 4 * off if off < 32768 else addr + 4 + 4 * (off - 65536)
+        if target >= addr:
+            continue
+        body = [x for x in ins if target <= x[0] <= addr]
+        if sum(1 for x in body if x[2].startswith("v_sin_f32")) >= 8:
+            loops.append((target, addr, body))
+    inner = [l for l in loops if not any(o is not l and l[0] <= o[0] and o[1] <= l[1] for o in loops)]
+    out = []
+    for start, _, body in sorted(inner, key=lambda l: l[0]):
+        eight = [x for x in body if x[1] == 8]
+        out.append({"kernel": kern, "start": start, "instrs": len(body), "bytes": sum(x[1] for x in body),
+                    "eight_byte": len(eight), "odd_dword": len([x for x in eight if x[0] % 8 != 0]),
+                    "sines": sum(1 for x in body if x[2].startswith("v_sin_f32"))})
+    return out
+
+
 # every shipped instantiation with a hardware-sine loop: fused forward (device noise / injected
 # noise, one sample per thread for few-frame launches), the harmonic-only fused backward
 SHIPPED = ("synth_frame_kernelILb1ELb0ELb0ELb0EE", "synth_frame_kernelILb0ELb0ELb0ELb0EE",
@@ -94,13 +120,13 @@ SHIPPED = ("synth_frame_kernelILb1ELb0ELb0ELb0EE", "synth_frame_kernelILb0ELb0EL
 
 
 def report(so, kern):
-    r = analyze(so, kern)
-    if r is None:
+    rs = analyze_all(so, kern)
+    if not rs:
         print(f"{so}: no sine loop in {kern}")
-    else:
+    for r in rs:
         print(f"{so.split('/')[-1]} {kern}: loop @{r['start']:#x} (mod 8 = {r['start'] % 8}), {r['instrs']} "
               f"instrs, {r['bytes']} B, {r['sines']} sines, 8-byte {r['eight_byte']}, at odd dwords {r['odd_dword']}")
-    return r
+    return rs
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     libs = [a for a in sys.argv[1:] if a.endswith(".so")] or [
