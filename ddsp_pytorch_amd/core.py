@@ -675,16 +675,26 @@ def mlp_block(x, linear, norm, act, out=None, extras=(), flags=0):
 
 
 def projections(x, lin1, lin2, pad_to=64):
-    """decoder.py:106-117 as ONE library GEMM: both layers' parameters stacked, fresh every call, into a
+    """decoder.py:106-117 in ONE launch: ddsp_hip_projections — both Linears on the bf16 matrix cores with the
+    fp32-accurate three-term split, reading each layer's parameters where they lie (at 512 inputs, 16-byte
+    aligned rows).  Elsewhere ONE library GEMM: both layers' parameters stacked, fresh every call, into a
     zero-padded [n_pad, K] buffer (ddsp_hip_stack_rows, one launch; n_pad a multiple of ``pad_to``:
     hipBLASLt runs 192 outputs in 28-30 us, the unpadded 166 in 38-39), then F.linear.  Returns the two
-    outputs as column slices of one [..., n_pad] result.  Nothing is cached on the modules."""
+    outputs as column slices of one [..., n] result.  Nothing is cached on the modules."""
     _dev(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
     n1, n2, K = lin1.out_features, lin2.out_features, x.shape[-1]
+    xc, w1, w2 = _c(x), _c(lin1.weight), _c(lin2.weight)
+    rows = xc.numel() // K if K else 0
+    n4 = -(-(n1 + n2) // 4) * 4  # row stride of the result: 16-byte aligned rows
+    y = torch.empty(*x.shape[:-1], n4, dtype=torch.float32, device=x.device)
+    st = _lib.call("projections", _lib.ptr(xc), K, K, _lib.ptr(w1), w1.stride(0), _lib.ptr(_c(lin1.bias)), n1,
+                   _lib.ptr(w2), w2.stride(0), _lib.ptr(_c(lin2.bias)), n2, _lib.ptr(y), n4, rows,
+                   _lib.stream_of(y), allow=(ERANGE,))
+    if st != ERANGE:
+        return y[..., :n1], y[..., n1:n1 + n2]
     n_pad = -(-(n1 + n2) // pad_to) * pad_to
     w = torch.empty(n_pad, K, dtype=torch.float32, device=x.device)
     b = torch.empty(n_pad, dtype=torch.float32, device=x.device)
-    w1, w2 = _c(lin1.weight), _c(lin2.weight)
     _lib.call("stack_rows", _lib.ptr(w1), w1.stride(0), _lib.ptr(_c(lin1.bias)), n1, _lib.ptr(w2), w2.stride(0),
               _lib.ptr(_c(lin2.bias)), n2, K, _lib.ptr(w), _lib.ptr(b), n_pad, _lib.stream_of(w))
     y = torch.nn.functional.linear(x, w, b)  # (this package's matrix-core projection kernel ran 40-44 us)

@@ -291,6 +291,16 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
 int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
                     const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream);
 
+/* decoder.py:106-117 (param = harmonic_proj(hidden), magnitudes = noise_proj(hidden)) in ONE launch on the bf16
+ * matrix cores with the fp32-accurate three-term split of ddsp_hip_linear, reading both layers' parameters where
+ * they lie (nn.Linear layout, W1 [n1, w1_ld], W2 [n2, w2_ld]): y[r][c] = x[r] W1[c]^T + b1[c] for c < n1 and
+ * x[r] W2[c - n1]^T + b2[c - n1] for n1 <= c < n1 + n2; columns of y past n1 + n2 are not written.  Replaces
+ * the two nn.Linear calls of decoder.py:106-117 (stack_rows + one library GEMM before).  in_features 512, x, W1,
+ * W2 16-byte aligned with ld % 4 == 0; else DDSP_HIP_ERANGE (callers keep their library GEMM). */
+int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, const float* w1, int64_t w1_ld,
+                         const float* b1, int64_t n1, const float* w2, int64_t w2_ld, const float* b2, int64_t n2,
+                         float* y, int64_t y_ld, int64_t rows, void* stream);
+
 /* decoder.py:106-117 (param = harmonic_proj(hidden), magnitudes = noise_proj(hidden)): the two projections'
  * parameters stacked into one zero-padded matrix w [n_pad, in_features] and
  * bias b [n_pad] (caller buffers; rows n1 + n2 .. n_pad - 1 zero), for one library GEMM over both at a

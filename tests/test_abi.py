@@ -118,6 +118,18 @@ def test_training_entry_points_reject_bad_arguments_without_launching():
                                                null, 1, 100, 10, null, 0, null) == EINVAL
     assert lib.ddsp_hip_reverb_backward_params(null, null, null, null, null, null, null, 0.0, null, null, null,
                                                null, -1, 100, 10, null, 0, null) == EINVAL
+    # the decoder's projections: missing parameters, a result narrower than both layers, K outside the kernel
+    assert lib.ddsp_hip_projections(null, 512, 512, null, 512, null, 101, null, 512, null, 65, null, 166, 10,
+                                    null) == EINVAL
+    assert lib.ddsp_hip_projections(null, 512, 512, null, 512, null, 101, null, 512, null, 65, null, 166, 0,
+                                    null) == EINVAL
+    dummy = ctypes.c_void_p(256)  # never dereferenced: every call below returns before any launch
+    assert lib.ddsp_hip_projections(dummy, 512, 512, dummy, 512, dummy, 101, dummy, 512, dummy, 65, dummy, 100, 10,
+                                    null) == EINVAL
+    assert lib.ddsp_hip_projections(dummy, 256, 256, dummy, 256, dummy, 101, dummy, 256, dummy, 65, dummy, 168, 10,
+                                    null) == ERANGE
+    assert lib.ddsp_hip_projections(dummy, 512, 512, dummy, 512, dummy, 101, dummy, 512, dummy, 65, dummy, 168, 0,
+                                    null) == 0
     # STFT: sizes outside the kernel's range, padding longer than the signal
     assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 100, 25, null) == ERANGE
     assert lib.ddsp_hip_stft_magnitude(null, null, 1, 1000, 8192, 2048, null) == ERANGE

@@ -135,7 +135,7 @@ def _assert_network_routes(spy, n_gru_inputs):
     assert spy.count("layer_norm_leaky_relu") >= 2, names  # the one-feature first blocks
     assert any(int(a[1]) == 512 and a[6].value is not None for n, a in spy.calls if n == "mlp_block"), \
         "out_mlp's extras (f0, loudness) path did not run"
-    assert spy.count("stack_rows") == 1, names  # both projections: one GEMM over their parameters stacked per call
+    assert spy.count("projections") == 1 and "stack_rows" not in names, names  # both projections: one launch
     assert spy.count("synth_frames_controls_prefix") == 1, names
     assert spy.count("reverb_forward") == 1, names  # the device-validated IR cache + UPOLS
 

@@ -100,15 +100,17 @@ def test_mlp_forward_extras_match_cat(dd):
 @pytest.mark.parametrize("K,n1,n2,rows", [(512, 101, 65, 12800), (512, 65, 65, 48), (512, 129, 65, 37),
                                           (64, 21, 17, 100), (32, 208, 16, 70)])
 def test_projections(dd, K, n1, n2, rows):
-    """decoder.py:106-117 as one GEMM over both layers' parameters stacked per call (core.projections)
-    against an fp64 host matmul."""
+    """decoder.py:106-117 as one launch (core.projections: ddsp_hip_projections at 512 inputs, else one GEMM over
+    both layers' parameters stacked per call) against an fp64 host matmul.  The two results are column slices
+    of one buffer with 16-byte aligned rows (the kernel route: n1 + n2 rounded up to 4; the GEMM route: to 64)."""
     torch.manual_seed(2)
     l1, l2 = torch.nn.Linear(K, n1).cuda(), torch.nn.Linear(K, n2).cuda()
     x = torch.randn(rows, K, device="cuda")
     with torch.no_grad():
         a, b = dd.core.projections(x, l1, l2)
     assert a.shape == (rows, n1) and b.shape == (rows, n2)
-    assert a.stride(0) == b.stride(0) and b.data_ptr() == a.data_ptr() + 4 * n1 and a.stride(0) % 64 == 0
+    assert a.stride(0) == b.stride(0) and b.data_ptr() == a.data_ptr() + 4 * n1
+    assert a.stride(0) == (-(-(n1 + n2) // 4) * 4 if K == 512 else -(-(n1 + n2) // 64) * 64)
     x64 = x.double().cpu()
     for got, lin in ((a, l1), (b, l2)):
         ref = x64 @ lin.weight.double().cpu().t() + lin.bias.double().cpu()
@@ -200,3 +202,49 @@ def test_linear_bf16x3(dd, rows, K, N):
     assert y.shape == (rows, N)
     assert rms(y.double() - ref) <= 2 * rms(y32.double() - ref) + 1e-12, (rms(y.double() - ref), rms(y32.double() - ref))
     assert float((y.double() - ref).abs().max()) <= 2 * float((y32.double() - ref).abs().max()) + 1e-12
+
+
+@pytest.mark.parametrize("rows,n1,n2,x_ld", [(12800, 101, 65, 512), (37, 101, 65, 512), (200, 129, 65, 516),
+                                              (64, 101, 0, 512), (130, 65, 300, 512)])
+def test_projections_bf16x3(dd, rows, n1, n2, x_ld):
+    """core.projections (ddsp_hip_projections: decoder.py:106-117's harmonic_proj and noise_proj in ONE launch,
+    each layer's parameters read where they lie) against an fp64 evaluation: within 2x of the f32 GEMMs'
+    (torch.addmm) error, RMS and max.  Ragged rows, a second 192-column block (129 + 65, 65 + 300), one layer
+    (n2 = 0, the second pointer set unused) and a row stride past the 512 features."""
+    torch.manual_seed(rows + n1 + n2)
+    xb = torch.randn(rows, x_ld, device="cuda") * 2.0
+    x = xb[:, :512]
+    lin1 = torch.nn.Linear(512, n1).cuda()
+    lin2 = torch.nn.Linear(512, n2).cuda()
+    with torch.no_grad():
+        p, m = dd.core.projections(x, lin1, lin2)
+        refs = [torch.addmm(l.bias.double(), x.double(), l.weight.double().t()) for l in (lin1, lin2)]
+        f32s = [torch.addmm(l.bias, x, l.weight.t()) for l in (lin1, lin2)]
+    assert p.shape == (rows, n1) and m.shape == (rows, n2)
+    rms = lambda e: float(e.pow(2).mean().sqrt()) if e.numel() else 0.0
+    for y, ref, y32 in zip((p, m), refs, f32s):
+        if not y.numel():
+            continue
+        e, e32 = y.double() - ref, y32.double() - ref
+        assert rms(e) <= 2 * rms(e32) + 1e-12, (rms(e), rms(e32))
+        assert float(e.abs().max()) <= 2 * float(e32.abs().max()) + 1e-12
+
+
+def test_projections_route_and_envelope(dd, monkeypatch):
+    """the projections take the one-launch kernel at 512 inputs (no stacking launch, no library GEMM) and fall
+    back to stack_rows + one GEMM outside it (256 inputs), with the same values"""
+    from ddsp_pytorch_amd import _lib
+    calls = []
+    real = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a, **k: calls.append(name) or real(name, *a, **k))
+    torch.manual_seed(3)
+    for K in (512, 256):
+        calls.clear()
+        x = torch.randn(300, K, device="cuda")
+        l1, l2 = torch.nn.Linear(K, 101).cuda(), torch.nn.Linear(K, 65).cuda()
+        with torch.no_grad():
+            p, m = dd.core.projections(x, l1, l2)
+            torch.testing.assert_close(p, l1(x), rtol=2e-5, atol=2e-5)
+            torch.testing.assert_close(m, l2(x), rtol=2e-5, atol=2e-5)
+        assert calls[0] == "projections"
+        assert ("stack_rows" in calls) == (K != 512), calls
