@@ -30,6 +30,19 @@ def save(name):
         for i, p in enumerate(parts):
             for j, t in enumerate(p.values() if isinstance(p, dict) else (p,)):
                 out[f"{key}_inject{i}_{j}"] = t.cpu()
+    # the reverb (forward transform + IR cache, MAC, inverse) and its backward (modules.Reverb under autograd)
+    from ddsp_pytorch_amd.synth import SynthPath
+    from ddsp_pytorch_amd.modules import Reverb
+    inp = make_inputs(64, 200, 100, 65, 512, device="cuda", with_noise=True)
+    path = SynthPath(512, 48000, reverb_length=48000).to("cuda")
+    out["reverb_path"] = path(inp["f0"], inp["param"], inp["mags"]).cpu()
+    torch.manual_seed(1)
+    rv = Reverb(48000, 48000).to("cuda")
+    x = (torch.randn(6, 40000, 1, device="cuda") * 0.3).requires_grad_(True)
+    y = rv(x)
+    y.backward(torch.randn_like(y))
+    out["reverb_y"], out["reverb_dx"] = y.detach().cpu(), x.grad.cpu()
+    out["reverb_dnoise"] = rv.noise.grad.cpu()
     os.makedirs("gpurun_out", exist_ok=True)
     torch.save(out, f"gpurun_out/bits_{name}.pt")
     print("saved", name, len(out), "tensors")
