@@ -680,69 +680,61 @@ __global__ void __launch_bounds__(512) linear_bf3_kernel(
 // decoder.py:106-117 — param = harmonic_proj(hidden), magnitudes = noise_proj(hidden) — as ONE launch on the
 // bf16 matrix cores with the fp32-accurate three-term split (the six products of linear_bf3_kernel), reading
 // both layers' parameters where they lie: output column c < n1 is W1 row c, n1 <= c < n1 + n2 is W2 row
-// c - n1.  K = 512 (the decoder's hidden size).  A workgroup: 64 rows x 192 columns (blockIdx.y: the
-// 192-column block), 8 waves as 2 row halves x 4 column groups of 48 (2 x 3 16 x 16 tiles per wave); x is split
-// once per workgroup into LDS planes a quarter of K at a time (linear_bf3_kernel's layout and pipeline), each
-// wave splits its own 48 W rows from a register ring.  At config 2 (12,800 x 512 -> 166) 200 workgroups,
-// one per CU, against hipBLASLt's 192-column GEMM after a stacking launch.
+// c - n1.  K = 512 (the decoder's hidden size).  A workgroup: 64 rows x 192 columns (blockIdx.y: the 192-column
+// block); x is split once per workgroup into LDS planes a quarter of K at a time (linear_bf3_kernel's layout and
+// pipeline).  The 8 waves are 4 column groups of 48 x 2 halves of K: wave (cg, kh) takes columns 48 cg .. + 47
+// for ALL 64 rows (4 x 3 tiles, 72 MFMAs per 32-wide chunk) over the chunks of parity kh, splitting its own W
+// rows from a register ring, so every W element is split once per workgroup; the kh = 1 half is added to the
+// kh = 0 half through LDS at the end (the x planes' space), one fp32 add per output.  At config 2 (12,800 x 512
+// -> 166) 200 workgroups, one per CU: 27.8 us against 32.1 us for 2 row halves x 4 column groups (each W
+// element split twice, 36 MFMAs per split) and 34.5 us for round 5's stacking launch + hipBLASLt GEMM
+// (profiles/r06y_projections_kernel.log).
 constexpr int kProjCols = 192;  // output columns per workgroup
-#ifndef DDSP_PROJ_RT
-#define DDSP_PROJ_RT 2
-#endif
-#ifndef DDSP_PROJ_KP
-#define DDSP_PROJ_KP 2
-#endif
-constexpr int kProjRT = DDSP_PROJ_RT;       // 16-row tiles per wave (a workgroup: 32 RT rows)
-constexpr int kProjRows = 32 * kProjRT;
-template <int RT, int kP>
-__global__ void __launch_bounds__(512) proj_bf3_kernel(
+__global__ void __launch_bounds__(512) proj_bf3_sk_kernel(
     const float* __restrict__ x, int64_t x_ld, const float* __restrict__ w1, int64_t w1_ld,
     const float* __restrict__ b1, int n1, const float* __restrict__ w2, int64_t w2_ld, const float* __restrict__ b2,
     int n2, float* __restrict__ y, int64_t y_ld, int64_t R) {
-  constexpr int K = 512, NQ = K / kBf3QK, NC = kBf3QK / 32, ROWS = 32 * RT;
-  constexpr int kPlane = ROWS * kBf3QK;  // bf16 elements per plane
-  __shared__ __attribute__((aligned(16))) uint32_t xs[2 * 3 * kPlane / 2];
+  constexpr int K = 512, NQ = K / kBf3QK, NC = kBf3QK / 32, kP = 2, NH = NQ * NC;
+  static_assert(NC == 2 * kP, "one ring slot per chunk parity step");
+  __shared__ __attribute__((aligned(16))) uint32_t xs[2 * 3 * kBf3Plane / 2];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int q = lane >> 4, l16 = lane & 15;
-  const int rg = wv & 1, cg = wv >> 1;  // rows 16 RT rg .. + 16 RT - 1, columns 48 cg .. + 47 of the block
-  const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+  const int kh = wv & 1, cg = wv >> 1;
+  const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
   const int c0 = blockIdx.y * kProjCols + 48 * cg;
   const int n = n1 + n2;
-  // W fragment of this lane for column tile j: column c0 + 16 j + l16, k = 32 h + 8 q .. + 7 (two float4);
-  // columns past n read W1 row 0 (their outputs are never stored)
   const float* wl[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = c0 + 16 * j + l16;
     wl[j] = (c < n1 ? w1 + (int64_t)c * w1_ld : c < n ? w2 + (int64_t)(c - n1) * w2_ld : w1) + 8 * q;
   }
+  // this wave's chunks: h = 2 s + kh, s = 0 .. NH / 2 - 1; ring slot s % kP
   float4 wb[kP][3][2];
 #pragma unroll
   for (int p = 0; p < kP; ++p)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      wb[p][j][0] = *reinterpret_cast<const float4*>(wl[j] + 32 * p);
-      wb[p][j][1] = *reinterpret_cast<const float4*>(wl[j] + 32 * p + 4);
+      wb[p][j][0] = *reinterpret_cast<const float4*>(wl[j] + 32 * (2 * p + kh));
+      wb[p][j][1] = *reinterpret_cast<const float4*>(wl[j] + 32 * (2 * p + kh) + 4);
     }
-  // split role: thread -> row t / (16 / RT), 8 RT k of a quarter (RT quads from Q = RT (t % (16 / RT)))
-  constexpr int TPR = 16 / RT;  // threads per row
-  const int srow = t / TPR, sq = RT * (t % TPR);
+  const int srow = t >> 3, sq = 2 * (t & 7);
   const float* xsrc = x + (r0 + srow < R ? r0 + srow : R - 1) * x_ld + 8 * sq;  // rows >= R: never stored
-  float4 xv[2 * RT];
+  float4 xv[4];
   auto load_quarter = [&](int qt) {
 #pragma unroll
-    for (int i = 0; i < 2 * RT; ++i) xv[i] = *reinterpret_cast<const float4*>(xsrc + kBf3QK * qt + 4 * i);
+    for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const float4*>(xsrc + kBf3QK * qt + 4 * i);
   };
   auto store_quarter = [&](int buf) {
-    uint32_t* base = xs + buf * (3 * kPlane / 2) + srow * (kBf3QK / 2);
+    uint32_t* base = xs + buf * (3 * kBf3Plane / 2) + srow * (kBf3QK / 2);
 #pragma unroll
-    for (int e = 0; e < RT; ++e) {
+    for (int e = 0; e < 2; ++e) {
       u32x4_t hq, mq, lq;
       split_bf16x3(xv[2 * e], xv[2 * e + 1], hq, mq, lq);
       const int pos = 4 * ((sq + e) ^ (srow & 15));  // uint32 offset of the quad
       *reinterpret_cast<u32x4_t*>(base + pos) = hq;
-      *reinterpret_cast<u32x4_t*>(base + kPlane / 2 + pos) = mq;
-      *reinterpret_cast<u32x4_t*>(base + kPlane + pos) = lq;
+      *reinterpret_cast<u32x4_t*>(base + kBf3Plane / 2 + pos) = mq;
+      *reinterpret_cast<u32x4_t*>(base + kBf3Plane + pos) = lq;
     }
   };
   load_quarter(0);
@@ -751,51 +743,47 @@ __global__ void __launch_bounds__(512) proj_bf3_kernel(
   store_quarter(1);
   load_quarter(2);  // in flight under quarter 0
   __syncthreads();
-  f32x4_t acc[RT][3];
+  f32x4_t acc[4][3];
 #pragma unroll
-  for (int i = 0; i < RT; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   for (int qt = 0; qt < NQ; ++qt) {
-    // rows 16 RT rg + 16 i + l16 of the buffer (row & 15 = l16)
-    const uint32_t* xb = xs + (qt & 1) * (3 * kPlane / 2) + (16 * RT * rg + l16) * (kBf3QK / 2);
+    const uint32_t* xb = xs + (qt & 1) * (3 * kBf3Plane / 2) + l16 * (kBf3QK / 2);  // row 16 i + l16: row & 15 = l16
 #pragma unroll
-    for (int cc = 0; cc < NC; cc += kP) {
+    for (int p = 0; p < kP; ++p) {
+      const int c = 2 * p + kh, h = qt * NC + c;
+      const int pos = 4 * ((4 * c + q) ^ l16);
+      u32x4_t xh[4], xm[4], xlo[4];
 #pragma unroll
-      for (int p = 0; p < kP; ++p) {
-        const int c = cc + p, h = qt * NC + c;
-        const int pos = 4 * ((4 * c + q) ^ l16);
-        u32x4_t xh[RT], xm[RT], xlo[RT];
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          const uint32_t* r = xb + 16 * i * (kBf3QK / 2) + pos;
-          xh[i] = *reinterpret_cast<const u32x4_t*>(r);
-          xm[i] = *reinterpret_cast<const u32x4_t*>(r + kPlane / 2);
-          xlo[i] = *reinterpret_cast<const u32x4_t*>(r + kPlane);
-        }
-        const int hn = h + kP < NQ * NC ? h + kP : NQ * NC - 1;  // clamped: the same loads every iteration
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          u32x4_t wh, wm, wlo;
-          split_bf16x3(wb[p][j][0], wb[p][j][1], wh, wm, wlo);
-#pragma unroll
-          for (int i = 0; i < RT; ++i) {  // small terms first
-            f32x4_t a = acc[i][j];
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wm), a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xlo[i]), as_bf16x8(wh), a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wlo), a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wh), a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wm), a, 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wh), a, 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          wb[p][j][0] = *reinterpret_cast<const float4*>(wl[j] + 32 * hn);
-          wb[p][j][1] = *reinterpret_cast<const float4*>(wl[j] + 32 * hn + 4);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the refill here (the scheduler would sink it to its use)
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t* r = xb + 16 * i * (kBf3QK / 2) + pos;
+        xh[i] = *reinterpret_cast<const u32x4_t*>(r);
+        xm[i] = *reinterpret_cast<const u32x4_t*>(r + kBf3Plane / 2);
+        xlo[i] = *reinterpret_cast<const u32x4_t*>(r + kBf3Plane);
       }
+      const int hn = h + 2 * kP < NH ? h + 2 * kP : NH - 2 + kh;  // clamped: the same loads every iteration
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        u32x4_t wh, wm, wlo;
+        split_bf16x3(wb[p][j][0], wb[p][j][1], wh, wm, wlo);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // small terms first
+          f32x4_t a = acc[i][j];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wm), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xlo[i]), as_bf16x8(wh), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wlo), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xm[i]), as_bf16x8(wh), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wm), a, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xh[i]), as_bf16x8(wh), a, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        wb[p][j][0] = *reinterpret_cast<const float4*>(wl[j] + 32 * hn);
+        wb[p][j][1] = *reinterpret_cast<const float4*>(wl[j] + 32 * hn + 4);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the refill here (the scheduler would sink it to its use)
     }
     if (qt + 1 < NQ) {
       __syncthreads();  // buffer qt & 1 fully read; the previous quarter's split writes visible
@@ -805,18 +793,31 @@ __global__ void __launch_bounds__(512) proj_bf3_kernel(
       }
     }
   }
-  // acc[i][j][e]: row 16 RT rg + 16 i + 4 q + e, column c0 + 16 j + l16
+  // the kh = 1 half through LDS ([cg][48 values][64 lanes] floats in the x planes' space)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs) + cg * 48 * 64 + lane;
+  if (kh == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[((3 * i + j) * 4 + e) * 64] = acc[i][j][e];
+  }
+  __syncthreads();
+  if (kh == 1) return;
+  // acc[i][j][e]: row 16 i + 4 q + e, column c0 + 16 j + l16
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = c0 + 16 * j + l16;
     if (c >= n) continue;
     const float cb = c < n1 ? b1[c] : b2[c - n1];
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t row = r0 + 16 * RT * rg + 16 * i + 4 * q + e;
-        if (row < R) y[row * y_ld + c] = acc[i][j][e] + cb;
+        const int64_t row = r0 + 16 * i + 4 * q + e;
+        if (row < R) y[row * y_ld + c] = (acc[i][j][e] + red[((3 * i + j) * 4 + e) * 64]) + cb;
       }
   }
 }
@@ -966,11 +967,11 @@ int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, cons
   }
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2);
   if (in_features != 512 || (al & 15) || (x_ld & 3) || (w1_ld & 3) || (w2_ld & 3) || n1 + n2 > 65535 * kProjCols ||
-      (rows + kProjRows - 1) / kProjRows > INT32_MAX)
+      (rows + kMlpRows - 1) / kMlpRows > INT32_MAX)
     return DDSP_HIP_ERANGE;  // callers keep their library GEMM
-  const dim3 grid((unsigned)((rows + kProjRows - 1) / kProjRows), (unsigned)((n1 + n2 + kProjCols - 1) / kProjCols));
-  hipLaunchKernelGGL((proj_bf3_kernel<kProjRT, DDSP_PROJ_KP>), grid, dim3(512), 0, reinterpret_cast<hipStream_t>(stream), x, x_ld, w1, w1_ld,
-                     b1, (int)n1, w2, w2_ld, b2, (int)n2, y, y_ld, rows);
+  const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows), (unsigned)((n1 + n2 + kProjCols - 1) / kProjCols));
+  hipLaunchKernelGGL(proj_bf3_sk_kernel, grid, dim3(512), 0, reinterpret_cast<hipStream_t>(stream), x, x_ld, w1, w1_ld, b1,
+                     (int)n1, w2, w2_ld, b2, (int)n2, y, y_ld, rows);
   return launch_status();
 }
 
