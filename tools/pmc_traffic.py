@@ -26,8 +26,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # reads the signal exactly once (26.2 MB) and reports 12.9 MB
 WIDE_READS = ("harmonic_samples_tiled_kernel", "upols_forward_kernel", "upols_forward_ir_kernel", "upols_inverse_kernel",
               "upols_mac_kernel", "upols_mac_ring_kernel", "upols_mac_stream_kernel")
-REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch of it
-    "synth_frame_kernel": ("synth_frame_kernel",),
+REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch of it (a name with its template
+    # arguments matches that instantiation only: bench.py's realtime leg launches the one-sample-per-thread
+    # instantiation of the fused kernel at 4 frames per call, whose launches must not dilute config 2's mean)
+    "synth_frame_kernel": ("synth_frame_kernel<true, false, false, false>",),
     "harmonic_frames_kernel": ("harmonic_frames_kernel",),
     "harmonic_samples_kernel": ("phase_chunk_sums_kernel", "harmonic_samples_tiled_kernel"),
     "filtered_noise_kernel": ("filtered_noise_kernel",),
@@ -37,9 +39,17 @@ REPORT = {  # bench.py roofline key -> kernels whose bytes add up to one launch 
 
 
 def short(name):
+    """kernel name with its template arguments, without namespace, return type and parameters"""
     base = name.replace("(anonymous namespace)", "anon").split("(")[0]
-    base = base.replace("void ", "").split("::")[-1]
-    return base.split("<")[0]
+    return base.replace("void ", "").split("::")[-1]
+
+
+def base(name):
+    return name.split("<")[0]
+
+
+def matches(k, pattern):
+    return k == pattern if "<" in pattern else base(k) == pattern
 
 
 def per_kernel(path):
@@ -63,14 +73,14 @@ def main():
     table = {}
     for k in sorted(set(fetch) | set(write)):
         f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
-        corr = 2.0 if k in WIDE_READS else 1.0
+        corr = 2.0 if base(k) in WIDE_READS else 1.0
         table[k] = {"fetch_kib_raw": round(f_kib, 1), "fetch_correction": corr,
                     "write_kib": round(w_kib, 1),
                     "hbm_bytes": int((f_kib * corr + w_kib) * 1024)}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(table, f, indent=1)
-    traffic = {key: sum(table[k]["hbm_bytes"] for k in ks if k in table) for key, ks in REPORT.items()
-               if any(k in table for k in ks)}
+    traffic = {key: sum(v["hbm_bytes"] for k, v in table.items() if any(matches(k, p) for p in ks))
+               for key, ks in REPORT.items() if any(matches(k, p) for k in table for p in ks)}
     traffic["_source"] = f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
