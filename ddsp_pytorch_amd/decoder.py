@@ -4,11 +4,12 @@ synth modules.
 
 The control network before the path runs at inference on gfx950 kernels
 too: each MLP block is one matrix-core launch with its LayerNorm + LeakyReLU (core.mlp_block), the
-GRU recurrence is the step kernel (core.gru; its input projection a hipBLASLt GEMM), the two
-projections one hipBLASLt GEMM over both layers' parameters stacked per call (core.projections), and the
-synthesis section of ``forward``
-(decoder.py:106-125) one fused launch before the reverb.  Under autograd the MLPs and projections
-keep torch's modules; the GRU's BPTT runs on its backward step kernel.
+GRU's input projection for every step one matrix-core launch (core.linear) and its recurrence one
+persistent launch per layer (core.gru), the two projections one matrix-core launch reading both layers'
+parameters in place (core.projections), and the synthesis section of ``forward`` (decoder.py:106-125) one
+fused launch before the reverb.  Under autograd the MLP blocks' Linears run their forward and input
+gradient on the matrix-core kernel (grad.LinearFn; LayerNorm, LeakyReLU and the weight gradients stay
+torch's), the projections are one differentiable GEMM, and the GRU's BPTT is one persistent launch.
 """
 import torch
 import torch.nn as nn
@@ -55,9 +56,17 @@ def _gru(mod, hidden, h0):
 
 def _mlp_fusable(seq, x):
     """An unobserved (Linear, LayerNorm, LeakyReLU) x n block chain (ddsp/core.py:122-129) on the GPU at
-    inference: the LayerNorm + LeakyReLU pairs may run as one kernel."""
+    inference (see _mlp_plain); the LayerNorm + LeakyReLU pairs may run as one kernel."""
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in seq.parameters())):
+        return False
+    return _mlp_plain(seq, x)
+
+
+def _mlp_plain(seq, x):
+    """An unobserved (Linear, LayerNorm, LeakyReLU) x n block chain (ddsp/core.py:122-129) in fp32 on the GPU:
+    no module or global hooks, the plain torch classes, affine LayerNorms, Linears with biases."""
     from torch.nn.modules import module as _m
-    if not x.is_cuda or torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in seq.parameters())):
+    if not x.is_cuda:
         return False
     if _m._global_forward_hooks or _m._global_forward_pre_hooks or seq._forward_hooks or seq._forward_pre_hooks:
         return False
@@ -86,7 +95,16 @@ def mlp_forward(seq, x, out=None, extras=()):
     kernel; the last block may write into ``out`` (e.g. a column slice of the GRU input concatenation)."""
     if not _mlp_fusable(seq, x):
         xin = torch.cat([x, *extras], -1) if extras else x
-        y = seq(xin)
+        if _mlp_plain(seq, xin):  # under autograd: each block's Linear on grad.LinearFn, the rest torch's
+            from .grad import LinearFn
+            y = xin
+            mods = list(seq)
+            for i in range(0, len(mods), 3):
+                lin, ln, act = mods[i:i + 3]
+                g = LinearFn.apply(y, lin.weight, lin.bias) if lin.in_features >= 16 else lin(y)
+                y = act(ln(g))
+        else:
+            y = seq(xin)
         if out is None:
             return y
         out.copy_(y)
@@ -131,7 +149,7 @@ def gru_decoder_forward(self, f0, loudness, z=None, realtime=False):
         for i, (m, x) in enumerate(mlps):
             mlp_forward(m, x, out=hidden[..., i * W:(i + 1) * W])
     else:
-        hidden = torch.cat([m(x) for m, x in mlps], -1)
+        hidden = torch.cat([mlp_forward(m, x) for m, x in mlps], -1)
     if realtime:
         gru_out, cache = _gru(self, hidden, self.cache_gru)
         self.cache_gru.copy_(cache)

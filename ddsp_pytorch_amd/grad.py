@@ -432,6 +432,36 @@ class StftMagFn(_F):
 GRU_BPTT_FLAGS = 0  # ddsp_hip_gru_backward_persistent's test hooks (core.GRU_*); 0 in use
 
 
+class LinearFn(_F):
+    """nn.Linear under autograd for the decoder's MLP blocks (ddsp/core.py:122-129, decoder.py:43-68): the
+    forward and the input gradient on ddsp_hip_linear (core.linear: the bf16 matrix cores with the exact
+    three-term split, fp32-accurate; torch.addmm outside its shapes) — y = x W^T + b and dx = dy W (the same
+    kernel over W^T) — the weight and bias gradients dW = dy^T x, db = sum dy on torch (hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        K = x.shape[-1]
+        x2 = core._c(x).reshape(-1, K)
+        y = core.linear(x2, weight, bias)
+        ctx.save_for_backward(x2, weight)
+        ctx.x_shape = x.shape
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        g2 = _g(gy).reshape(-1, w.shape[0])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            wt = w.t().contiguous()
+            gx = core.linear(g2, wt, torch.zeros(wt.shape[0], dtype=wt.dtype, device=wt.device)).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            gw = g2.t().mm(x2)
+        if ctx.needs_input_grad[2]:
+            gb = g2.sum(0)
+        return gx, gw, gb
+
+
 class GRUFn(_F):
     """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 step kernels
     (csrc/gru.hip); the input projection and the weight gradients are plain GEMMs."""

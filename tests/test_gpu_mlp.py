@@ -248,3 +248,53 @@ def test_projections_route_and_envelope(dd, monkeypatch):
             torch.testing.assert_close(m, l2(x), rtol=2e-5, atol=2e-5)
         assert calls[0] == "projections"
         assert ("stack_rows" in calls) == (K != 512), calls
+
+
+@pytest.mark.parametrize("rows,K,N", [(12800, 512, 512), (300, 1024, 512), (77, 514, 512)])
+def test_linear_fn_autograd(dd, rows, K, N):
+    """grad.LinearFn (the decoder's MLP Linears under autograd: forward and input gradient on ddsp_hip_linear,
+    weight / bias gradients on torch) against an fp64 evaluation: output and all three gradients within 2x
+    of torch's fp32 Linear's error.  K = 514 (the out_mlp's first block) runs torch's GEMMs inside it."""
+    from ddsp_pytorch_amd.grad import LinearFn
+    torch.manual_seed(rows + K)
+    lin = torch.nn.Linear(K, N).cuda()
+    x = torch.randn(rows, K, device="cuda", requires_grad=True)
+    gy = torch.randn(rows, N, device="cuda")
+    res = {}
+    for name, fn in (("ours", lambda a, w, b: LinearFn.apply(a, w, b)),
+                     ("f32", torch.nn.functional.linear)):
+        xi = x.detach().clone().requires_grad_(True)
+        w = lin.weight.detach().clone().requires_grad_(True)
+        b = lin.bias.detach().clone().requires_grad_(True)
+        y = fn(xi, w, b)
+        y.backward(gy)
+        res[name] = (y.detach(), xi.grad, w.grad, b.grad)
+    xd, wd, bd = x.detach().double(), lin.weight.detach().double(), lin.bias.detach().double()
+    ref = (xd @ wd.t() + bd, gy.double() @ wd, gy.double().t() @ xd, gy.double().sum(0))
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    for ours, f32, r in zip(res["ours"], res["f32"], ref):
+        assert rms(ours.double() - r) <= 2 * rms(f32.double() - r) + 1e-12, (rms(ours.double() - r), rms(f32.double() - r))
+
+
+def test_mlp_autograd_route(dd, monkeypatch):
+    """Under autograd the decoder's MLPs (mlp_forward) run each block's Linear on LinearFn — the 512-input blocks'
+    forward and input gradient on the matrix-core kernel — and match torch's modules (values and every
+    parameter's gradient) to fp32 accuracy; the one-feature first block stays torch's Linear."""
+    from ddsp_pytorch_amd import _lib
+    from ddsp_pytorch_amd.decoder import mlp, mlp_forward
+    calls = []
+    real = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a, **k: calls.append(name) or real(name, *a, **k))
+    torch.manual_seed(11)
+    seq = mlp(1, 512, 3).cuda()
+    x = torch.randn(8, 200, 1, device="cuda")
+    y = mlp_forward(seq, x)
+    y.pow(2).mean().backward()
+    ours = [p.grad.clone() for p in seq.parameters()]
+    assert calls.count("linear") == 4, calls  # blocks 2 and 3: forward + input gradient each
+    seq.zero_grad()
+    y_ref = seq(x)
+    y_ref.pow(2).mean().backward()
+    torch.testing.assert_close(y, y_ref, rtol=1e-5, atol=1e-5)
+    for g, p in zip(ours, seq.parameters()):
+        torch.testing.assert_close(g, p.grad, rtol=1e-4, atol=1e-6)
