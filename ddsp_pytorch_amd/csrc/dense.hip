@@ -939,12 +939,16 @@ int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const flo
   if (rows == 0) return DDSP_HIP_OK;
   if (!x || !y || x_ld < in_features || w_ld < in_features || y_ld < out_features) return DDSP_HIP_EINVAL;
   const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
-  if ((in_features != 512 && in_features != 1024) || out_features % kMlpN || (al & 15) || (x_ld & 3) || (w_ld & 3) ||
+  if ((in_features != 512 && in_features != 1024 && in_features != 1536) || out_features % kMlpN || (al & 15) ||
+      (x_ld & 3) || (w_ld & 3) ||
       (rows + kMlpRows - 1) / kMlpRows > INT32_MAX || out_features / kMlpN > 65535)
     return DDSP_HIP_ERANGE;  // callers keep their library GEMM
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows), (unsigned)(out_features / kMlpN));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (in_features == 1024)
+  if (in_features == 1536)  // the GRU input gradient (3 gates x 512 -> 1024 under autograd)
+    hipLaunchKernelGGL((linear_bf3_kernel<2, 1536, false>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, nullptr,
+                       nullptr, 0, nullptr, nullptr, 0.0f, 0.0f, y, y_ld, rows);
+  else if (in_features == 1024)
     hipLaunchKernelGGL((linear_bf3_kernel<2, 1024, false>), grid, dim3(512), 0, st, x, x_ld, w, w_ld, bias, nullptr,
                        nullptr, 0, nullptr, nullptr, 0.0f, 0.0f, y, y_ld, rows);
   else

@@ -463,8 +463,9 @@ class LinearFn(_F):
 
 
 class GRUFn(_F):
-    """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 step kernels
-    (csrc/gru.hip); the input projection and the weight gradients are plain GEMMs."""
+    """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 kernels (csrc/gru.hip); the input
+    projection and its input gradient on the matrix-core linear kernel (core.linear), the weight gradients
+    plain GEMMs."""
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0):
@@ -506,7 +507,10 @@ class GRUFn(_F):
         dG = torch.cat([dxp[..., :2 * H], dgn], -1).view(B * T, 3 * H)
         hprev = torch.cat([(h0p.view(B, 1, H) if h0p is not None else torch.zeros(B, 1, H, device=x.device)),
                            out[:, :-1]], 1).reshape(B * T, H)
-        dx = (dxp2 @ w_ih).view(B, T, I) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:  # dx = dxp W_ih on the matrix-core kernel (W_ih^T as its weight; addmm outside it)
+            wt = w_ih.t().contiguous()
+            dx = core.linear(dxp2, wt, torch.zeros(wt.shape[0], dtype=wt.dtype, device=wt.device)).view(B, T, I)
         dw_ih = dxp2.t() @ x.reshape(B * T, I) if ctx.needs_input_grad[1] else None
         dw_hh = dG.t() @ hprev if ctx.needs_input_grad[2] else None
         db_ih = dxp2.sum(0) if ctx.needs_input_grad[3] else None

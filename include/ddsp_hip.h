@@ -286,8 +286,10 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
 /* A Linear y = x W^T + b (W [out_features, w_ld], the nn.Linear / nn.GRU weight layout) on the bf16 matrix cores
  * with the fp32-accurate three-term split of ddsp_hip_mlp_block: the decoder's GRU input projection for every
  * step at once (decoder.py:41, torch.nn.GRU's x W_ih^T + b_ih; 12,800 x 1024 -> 1536 at config 2).
- * in_features 512 or 1024, out_features a multiple of 512, x and W 16-byte aligned with ld % 4 == 0; else
- * DDSP_HIP_ERANGE (callers keep their library GEMM). */
+ * Under autograd also the input gradient of the MLP blocks' Linears (dx = dy W, W^T as the weight) and of the
+ * GRU's input projection (in_features 1536 = 3 gates x 512).  in_features 512, 1024 or 1536, out_features a
+ * multiple of 512, x and W 16-byte aligned with ld % 4 == 0; else DDSP_HIP_ERANGE (callers keep their library
+ * GEMM). */
 int ddsp_hip_linear(const float* x, int64_t x_ld, int64_t in_features, const float* w, int64_t w_ld,
                     const float* bias, float* y, int64_t y_ld, int64_t rows, int64_t out_features, void* stream);
 
