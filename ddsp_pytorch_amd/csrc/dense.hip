@@ -234,6 +234,122 @@ __global__ void __launch_bounds__(256) ln_leaky_kernel(const float* __restrict__
   }
 }
 
+// Backward of ln_leaky_kernel (training: the MLP blocks' LayerNorm + LeakyReLU, ddsp/core.py:122-129, under
+// autograd).  Per row, from the saved pre-activation x: mean / rstd as the forward forms them, n = (x - mean) rstd,
+// z = n gamma + beta (the forward's expression, so the LeakyReLU's branch is the forward's), dz = dy (z > 0 ? 1 :
+// slope) (torch's leaky_relu_backward), dn = dz gamma, dx = rstd (dn - mean(dn) - n mean(dn n)) (torch's
+// layer_norm backward for the biased variance).  One wave per row over a fixed grid (rows w, w + 4 gridDim, ...), so
+// each lane keeps its columns' dgamma = sum dz n and dbeta = sum dz in registers; the workgroup's 4 waves are summed
+// in LDS into one partial per workgroup, and ln_leaky_bwd_sum_kernel adds the partials in workgroup order
+// (deterministic, no atomics).
+constexpr int kLnBwdGrid = 256;
+template <int V4>
+__global__ void __launch_bounds__(256) ln_leaky_bwd_kernel(const float* __restrict__ x, int64_t x_ld,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           float eps, float slope, const float* __restrict__ dy,
+                                                           int64_t dy_ld, float* __restrict__ dx, int64_t dx_ld,
+                                                           float* __restrict__ part, int64_t rows) {
+  constexpr int C = 256 * V4;
+  __shared__ float4 red[4][2][64 * V4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float4 gm[V4], bt[V4], dgs[V4], dbs[V4];
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    gm[i] = reinterpret_cast<const float4*>(gamma)[lane + 64 * i];
+    bt[i] = reinterpret_cast<const float4*>(beta)[lane + 64 * i];
+    dgs[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    dbs[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+    float4 v[V4], d[V4];
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      v[i] = reinterpret_cast<const float4*>(x + row * x_ld)[lane + 64 * i];
+      d[i] = reinterpret_cast<const float4*>(dy + row * dy_ld)[lane + 64 * i];
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mean = wave_sum(s) * (1.0f / (float)C);
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+      q += (a * a + b * b) + (c * c + e * e);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / (float)C) + eps);
+    float nn[4 * V4], dn[4 * V4];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < V4; ++i) {
+      const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w}, dd[4] = {d[i].x, d[i].y, d[i].z, d[i].w};
+      const float gg[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w}, bb[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
+      float dz[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float n = (vv[e] - mean) * rstd;
+        const float z = n * gg[e] + bb[e];
+        dz[e] = z > 0.0f ? dd[e] : dd[e] * slope;
+        nn[4 * i + e] = n;
+        dn[4 * i + e] = dz[e] * gg[e];
+        s1 += dn[4 * i + e];
+        s2 += dn[4 * i + e] * n;
+      }
+      dgs[i] = make_float4(dgs[i].x + dz[0] * nn[4 * i], dgs[i].y + dz[1] * nn[4 * i + 1],
+                           dgs[i].z + dz[2] * nn[4 * i + 2], dgs[i].w + dz[3] * nn[4 * i + 3]);
+      dbs[i] = make_float4(dbs[i].x + dz[0], dbs[i].y + dz[1], dbs[i].z + dz[2], dbs[i].w + dz[3]);
+    }
+    const float m1 = wave_sum(s1) * (1.0f / (float)C), m2 = wave_sum(s2) * (1.0f / (float)C);
+    float4* dr = reinterpret_cast<float4*>(dx + row * dx_ld);
+#pragma unroll
+    for (int i = 0; i < V4; ++i)
+      dr[lane + 64 * i] = make_float4(rstd * (dn[4 * i] - m1 - nn[4 * i] * m2), rstd * (dn[4 * i + 1] - m1 - nn[4 * i + 1] * m2),
+                                      rstd * (dn[4 * i + 2] - m1 - nn[4 * i + 2] * m2),
+                                      rstd * (dn[4 * i + 3] - m1 - nn[4 * i + 3] * m2));
+  }
+  if (!part) return;
+#pragma unroll
+  for (int i = 0; i < V4; ++i) {
+    red[w][0][lane + 64 * i] = dgs[i];
+    red[w][1][lane + 64 * i] = dbs[i];
+  }
+  __syncthreads();
+  // thread t sums the 4 waves for float4 slot t of [dgamma | dbeta] (2 * 64 V4 slots)
+  for (int t = threadIdx.x; t < 2 * 64 * V4; t += 256) {
+    const int h = t / (64 * V4), k = t - h * (64 * V4);
+    float4 a = red[0][h][k];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const float4 b = red[ww][h][k];
+      a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * C + h * C)[k] = a;
+  }
+}
+
+// [dgamma | dbeta][c] = sum over the workgroups' partials: a workgroup per 64 columns, its 4 waves summing the
+// partials j, j + 4, ... (coalesced over the 64 columns), then the 4 wave sums in wave order (deterministic)
+__global__ void __launch_bounds__(256) ln_leaky_bwd_sum_kernel(const float* __restrict__ part, int nparts, int C,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a = 0.0f;
+  if (c < 2 * C) {
+#pragma unroll 8
+    for (int b = w; b < nparts; b += 4) a += part[(int64_t)b * 2 * C + c];
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w != 0 || c >= 2 * C) return;
+  const float s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (c < C) {
+    if (dgamma) dgamma[c] = s;
+  } else if (dbeta) {
+    dbeta[c - C] = s;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // One whole MLP block at full batch (ddsp/core.py:122-129): y = LeakyReLU(LayerNorm(x W^T + b)) for
 // 512 output features, the Linear on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
@@ -890,6 +1006,45 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
     hipLaunchKernelGGL(ln_leaky_kernel<2>, grid, dim3(256), 0, st, x, x_ld, w1, b1, gamma, beta, eps, slope, y, y_ld, rows);
   else
     hipLaunchKernelGGL(ln_leaky_kernel<4>, grid, dim3(256), 0, st, x, x_ld, w1, b1, gamma, beta, eps, slope, y, y_ld, rows);
+  return launch_status();
+}
+
+size_t ddsp_hip_layer_norm_leaky_relu_backward_workspace_size(int64_t cols) {
+  return cols > 0 ? sizeof(float) * (size_t)kLnBwdGrid * 2 * (size_t)cols : 0;
+}
+
+int ddsp_hip_layer_norm_leaky_relu_backward(const float* x, int64_t x_ld, const float* gamma, const float* beta, float eps,
+                                            float slope, const float* grad_y, int64_t dy_ld, float* grad_x, int64_t dx_ld,
+                                            float* grad_gamma, float* grad_beta, int64_t rows, int64_t cols, void* ws,
+                                            size_t ws_bytes, void* stream) {
+  if (rows < 0 || cols < 1 || !gamma || !beta) return DDSP_HIP_EINVAL;
+  if (rows == 0) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (grad_gamma && hipMemsetAsync(grad_gamma, 0, sizeof(float) * (size_t)cols, st) != hipSuccess) return DDSP_HIP_ELAUNCH;
+    if (grad_beta && hipMemsetAsync(grad_beta, 0, sizeof(float) * (size_t)cols, st) != hipSuccess) return DDSP_HIP_ELAUNCH;
+    return DDSP_HIP_OK;
+  }
+  if (!x || !grad_y || !grad_x || x_ld < cols || dy_ld < cols || dx_ld < cols) return DDSP_HIP_EINVAL;
+  const bool params = grad_gamma || grad_beta;
+  if (params && (!ws || ws_bytes < ddsp_hip_layer_norm_leaky_relu_backward_workspace_size(cols))) return DDSP_HIP_EWORKSPACE;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad_y) |
+                       reinterpret_cast<uintptr_t>(grad_x) | reinterpret_cast<uintptr_t>(gamma) |
+                       reinterpret_cast<uintptr_t>(beta);
+  if ((cols != 512 && cols != 1024) || (al & 15) || (x_ld & 3) || (dy_ld & 3) || (dx_ld & 3))
+    return DDSP_HIP_ERANGE;  // callers keep torch's LayerNorm + LeakyReLU backward
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* part = params ? reinterpret_cast<float*>(ws) : nullptr;
+  const int64_t need = (rows + 3) / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(kLnBwdGrid, need);
+  if (cols == 512)
+    hipLaunchKernelGGL(ln_leaky_bwd_kernel<2>, dim3(grid), dim3(256), 0, st, x, x_ld, gamma, beta, eps, slope, grad_y,
+                       dy_ld, grad_x, dx_ld, part, rows);
+  else
+    hipLaunchKernelGGL(ln_leaky_bwd_kernel<4>, dim3(grid), dim3(256), 0, st, x, x_ld, gamma, beta, eps, slope, grad_y,
+                       dy_ld, grad_x, dx_ld, part, rows);
+  if (params)
+    hipLaunchKernelGGL(ln_leaky_bwd_sum_kernel, dim3((unsigned)((2 * cols + 63) / 64)), dim3(256), 0, st, part,
+                       (int)grid, (int)cols, grad_gamma, grad_beta);
   return launch_status();
 }
 

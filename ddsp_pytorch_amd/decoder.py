@@ -95,14 +95,19 @@ def mlp_forward(seq, x, out=None, extras=()):
     kernel; the last block may write into ``out`` (e.g. a column slice of the GRU input concatenation)."""
     if not _mlp_fusable(seq, x):
         xin = torch.cat([x, *extras], -1) if extras else x
-        if _mlp_plain(seq, xin):  # under autograd: each block's Linear on grad.LinearFn, the rest torch's
-            from .grad import LinearFn
+        if _mlp_plain(seq, xin):
+            # under autograd: each block's Linear on grad.LinearFn (the one-feature first Linear stays torch's) and
+            # its LayerNorm + LeakyReLU on grad.LNLeakyFn (512 / 1024 features; else torch's modules)
+            from .grad import LinearFn, LNLeakyFn
             y = xin
             mods = list(seq)
             for i in range(0, len(mods), 3):
                 lin, ln, act = mods[i:i + 3]
                 g = LinearFn.apply(y, lin.weight, lin.bias) if lin.in_features >= 16 else lin(y)
-                y = act(ln(g))
+                if lin.out_features in (512, 1024) and tuple(ln.normalized_shape) == (lin.out_features,):
+                    y = LNLeakyFn.apply(g, ln.weight, ln.bias, ln.eps, act.negative_slope)
+                else:
+                    y = act(ln(g))
         else:
             y = seq(xin)
         if out is None:

@@ -462,6 +462,41 @@ class LinearFn(_F):
         return gx, gw, gb
 
 
+class LNLeakyFn(_F):
+    """LeakyReLU(LayerNorm(g)) under autograd for the decoder's MLP blocks (ddsp/core.py:122-129): the forward on
+    ddsp_hip_layer_norm_leaky_relu, the backward — dg, dgamma, dbeta from the saved g — on
+    ddsp_hip_layer_norm_leaky_relu_backward (one pass instead of torch's LeakyReLU and LayerNorm backward kernels
+    and its separate parameter-gradient reductions).  g [..., cols] with cols 512 or 1024 (mlp_forward checks)."""
+
+    @staticmethod
+    def forward(ctx, g, gamma, beta, eps, slope):
+        gc = core._c(g)
+        cols = gc.shape[-1]
+        rows = gc.numel() // cols
+        y = torch.empty_like(gc)
+        _lib.call("layer_norm_leaky_relu", _lib.ptr(gc), cols, None, None, _lib.ptr(core._c(gamma)),
+                  _lib.ptr(core._c(beta)), float(eps), float(slope), _lib.ptr(y), cols, rows, cols, _lib.stream_of(y))
+        ctx.save_for_backward(gc, gamma, beta)
+        ctx.eps, ctx.slope = float(eps), float(slope)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        gc, gamma, beta = ctx.saved_tensors
+        cols = gc.shape[-1]
+        rows = gc.numel() // cols
+        dy = _g(gy)
+        dg = torch.empty_like(gc)  # (the kernel always writes it)
+        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dgam = torch.empty_like(gamma) if ctx.needs_input_grad[1] else None
+        dbet = torch.empty_like(beta) if ctx.needs_input_grad[2] else None
+        ws = core._workspace(_lib.query("layer_norm_leaky_relu_backward_workspace_size", cols), gc.device) if want else None
+        _lib.call("layer_norm_leaky_relu_backward", _lib.ptr(gc), cols, _lib.ptr(core._c(gamma)), _lib.ptr(core._c(beta)),
+                  ctx.eps, ctx.slope, _lib.ptr(dy), cols, _lib.ptr(dg), cols, _lib.ptr(dgam), _lib.ptr(dbet), rows, cols,
+                  _lib.ptr(ws), ws.numel() if ws is not None else 0, _lib.stream_of(dg))
+        return (dg if ctx.needs_input_grad[0] else None), dgam, dbet, None, None
+
+
 class GRUFn(_F):
     """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 kernels (csrc/gru.hip); the input
     projection and its input gradient on the matrix-core linear kernel (core.linear), the weight gradients

@@ -283,6 +283,18 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
                                    const float* beta, float eps, float slope, float* y, int64_t y_ld, int64_t rows,
                                    int64_t cols, void* stream);
 
+/* Backward of ddsp_hip_layer_norm_leaky_relu without w1 (training: the MLP blocks' LayerNorm + LeakyReLU,
+ * core.py:122-129, replacing torch's leaky_relu_backward + native_layer_norm_backward): from the pre-activation x
+ * [rows, x_ld] and grad_y, grad_x [rows, dx_ld] and (each nullable) grad_gamma / grad_beta [cols], the column sums
+ * over all rows (deterministic order).  The LeakyReLU's branch is taken on z = LayerNorm(x) formed as the forward
+ * forms it.  ws: ddsp_hip_layer_norm_leaky_relu_backward_workspace_size(cols) bytes when a parameter gradient is
+ * requested.  cols 512 or 1024 with 16-byte aligned rows, else DDSP_HIP_ERANGE. */
+size_t ddsp_hip_layer_norm_leaky_relu_backward_workspace_size(int64_t cols);
+int ddsp_hip_layer_norm_leaky_relu_backward(const float* x, int64_t x_ld, const float* gamma, const float* beta, float eps,
+                                            float slope, const float* grad_y, int64_t dy_ld, float* grad_x, int64_t dx_ld,
+                                            float* grad_gamma, float* grad_beta, int64_t rows, int64_t cols, void* ws,
+                                            size_t ws_bytes, void* stream);
+
 /* A Linear y = x W^T + b (W [out_features, w_ld], the nn.Linear / nn.GRU weight layout) on the bf16 matrix cores
  * with the fp32-accurate three-term split of ddsp_hip_mlp_block: the decoder's GRU input projection for every
  * step at once (decoder.py:41, torch.nn.GRU's x W_ih^T + b_ih; 12,800 x 1024 -> 1536 at config 2).

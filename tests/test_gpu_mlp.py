@@ -295,9 +295,40 @@ def test_mlp_autograd_route(dd, monkeypatch):
     y.pow(2).mean().backward()
     ours = [p.grad.clone() for p in seq.parameters()]
     assert calls.count("linear") == 4, calls  # blocks 2 and 3: forward + input gradient each
+    assert calls.count("layer_norm_leaky_relu") == 3 and calls.count("layer_norm_leaky_relu_backward") == 3, calls
     seq.zero_grad()
     y_ref = seq(x)
     y_ref.pow(2).mean().backward()
     torch.testing.assert_close(y, y_ref, rtol=1e-5, atol=1e-5)
     for g, p in zip(ours, seq.parameters()):
         torch.testing.assert_close(g, p.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("rows,cols", [(12800, 512), (37, 512), (300, 1024)])
+def test_ln_leaky_fn_autograd(dd, rows, cols):
+    """grad.LNLeakyFn (LeakyReLU(LayerNorm(g)) under autograd: one forward kernel, one backward pass plus the
+    parameter-gradient sums) against torch's modules evaluated in fp64: the output and the gradients w.r.t. g,
+    gamma and beta within 2x (+ a small floor) of torch's fp32 modules' error."""
+    from ddsp_pytorch_amd.grad import LNLeakyFn
+    torch.manual_seed(rows + cols)
+    ln = torch.nn.LayerNorm(cols).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.3 * torch.randn(cols))
+        ln.bias.copy_(0.2 * torch.randn(cols))
+    g = torch.randn(rows, cols, device="cuda") * 1.7 + 0.4
+    gy = torch.randn(rows, cols, device="cuda")
+    res = {}
+    for name in ("ours", "f32", "f64"):
+        dt = torch.float64 if name == "f64" else torch.float32
+        gi = g.detach().to(dt).requires_grad_(True)
+        w = ln.weight.detach().to(dt).requires_grad_(True)
+        b = ln.bias.detach().to(dt).requires_grad_(True)
+        if name == "ours":
+            y = LNLeakyFn.apply(gi, w, b, ln.eps, 0.01)
+        else:
+            y = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(gi, (cols,), w, b, ln.eps), 0.01)
+        y.backward(gy.to(dt))
+        res[name] = [t.double() for t in (y.detach(), gi.grad, w.grad, b.grad)]
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    for ours, f32, ref in zip(res["ours"], res["f32"], res["f64"]):
+        assert rms(ours - ref) <= 2 * rms(f32 - ref) + 1e-7 * (1 + rms(ref)), (rms(ours - ref), rms(f32 - ref))
