@@ -749,6 +749,23 @@ def main():
                              "note": "SURVEY 8(d) convention: op-boundary bytes / fused-kernel time; "
                                      "exceeds HBM peak because fusion removed that traffic"}
 
+    # the reverb group (forward transform + IR-cache check, MAC, inverse) against HBM: SURVEY 8(d)'s 8 B per
+    # sample (x in, y out) over the group's event-timed duration, beside its PMC bytes (the two spectra round
+    # trips of the partitioned convolution, DESIGN.md 3a, make the physical traffic ~5x the algorithmic bytes)
+    roofline_reverb = None
+    if syn.reverb is not None and kern_ms.get("reverb"):
+        rev_s = kern_ms["reverb"] * 1e-3
+        rev_bytes = 8 * B * F * bs
+        rt = traffic.get("reverb")
+        roofline_reverb = {"bound": "hbm", "achieved": round(rev_bytes / rev_s / 1e9, 1), "peak": 8000.0,
+                           "unit": "GB/s", "frac": round(rev_bytes / rev_s / 8e12, 4), "traffic": rt,
+                           "physical_gbs": round(rt / rev_s / 1e9, 1) if rt else None,
+                           "algorithmic_bytes_per_launch": rev_bytes, "avg_group_ms": round(kern_ms["reverb"], 4),
+                           "kernels": "upols_forward_ir_kernel + upols_mac_stream_kernel + upols_inverse_kernel",
+                           "note": "8 B/sample (x in, y out; the cached IR spectrum aside) over the group's "
+                                   "event-timed duration (kernel_ms.reverb); traffic = PMC FETCH_SIZE + WRITE_SIZE "
+                                   "per group (profiles/pmc_traffic.json)"}
+
     result = {
         "metric": "audio samples/sec (48 kHz, 100 harm, blk=512) at 1/2/4/8 GPU; % HBM roofline",
         "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -761,6 +778,7 @@ def main():
                    "global_batch": B * world, "seq_len": F * bs, "parallelism": f"batch-shard x{world}"},
         "roofline": roofline,
         "op_boundary_effective": op_boundary_effective,
+        "roofline_reverb": roofline_reverb,
         "kernel_ms": {k: round(v, 4) for k, v in kern_ms.items()},
         "kernel_ms_note": "HIP events, one kernel group per loop, measured after the timed region; "
                           "roofline.avg_launch_ms is from inside it.  The synthesis kernel's time depends "
