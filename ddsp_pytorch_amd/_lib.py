@@ -81,6 +81,8 @@ SIGNATURES = {
     "ddsp_hip_linear": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_layer_norm_leaky_relu": (_I, [_P, _I64, _P, _P, _P, _P, _F, _F, _P, _I64, _I64, _I64, _P]),
     "ddsp_hip_layer_norm_leaky_relu_backward_workspace_size": (_SZ, [_I64]),
+    "ddsp_hip_linear_weight_grad_workspace_size": (_SZ, [_I64, _I64, _I64]),
+    "ddsp_hip_linear_weight_grad": (_I, [_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_layer_norm_leaky_relu_backward": (_I, [_P, _I64, _P, _P, _F, _F, _P, _I64, _P, _I64, _P, _P, _I64, _I64, _P, _SZ, _P]),
     "ddsp_hip_projections": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _P]),
     "ddsp_hip_stack_rows": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P, _I64, _P]),

@@ -938,6 +938,155 @@ __global__ void __launch_bounds__(512) proj_bf3_sk_kernel(
   }
 }
 
+// Weight gradient of a Linear under autograd (training: the decoder MLPs' Linears, the GRU's W_ih / W_hh):
+// dW[m][n] = sum_r dY[r][m] X[r][n] — a product over the ROW index of two row-major matrices, on the bf16 matrix
+// cores with the exact three-term split (six products, fp32-accurate).  A workgroup: a 64 (m) x 128 (n) tile of dW
+// over one of S row ranges (split-K; the S per-tile partials are summed in range order by wgrad_sum_kernel, so the
+// result does not depend on scheduling).  Per 32-row chunk each thread loads 8 consecutive rows of one column
+// (coalesced across the wave's lanes), splits them and writes the 16-byte [column][8 rows] quads of the three
+// planes into LDS — the MFMA fragments' k-major layout, quads swizzled per column so that a fragment read is
+// conflict-free — double-buffered with one barrier per chunk; the loads run two chunks ahead (two register sets)
+// under the current chunk's 48 MFMAs per wave (wave w: m-tile w x the 8 n-tiles).  Row ranges are sliced by XCD
+// (S a multiple of 8, workgroup b on XCD b % 8 takes ranges of slice b % 8): an XCD streams only its eighth of
+// dY and X from HBM and serves the tiles' re-reads from its own L2.
+constexpr int kWgM = 64, kWgN = 128, kWgR = 32;
+__device__ __forceinline__ int wgrad_quad(int col, int q) { return col * (kWgR / 8) + (q ^ ((0x78 >> (2 * ((col >> 2) & 3))) & 3)); }
+struct WgradRegs {
+  float a[8], b[2][8];
+};
+__global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict__ dy, int64_t dy_ld,
+                                                        const float* __restrict__ x, int64_t x_ld,
+                                                        float* __restrict__ part, int64_t R, int M, int N, int S,
+                                                        int64_t rows_per_split) {
+  // [buffer][plane][column][32 rows] bf16: A (dY) 64 columns, B (X) 128 columns
+  __shared__ __attribute__((aligned(16))) uint32_t la[2][3][kWgM * kWgR / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t lb[2][3][kWgN * kWgR / 2];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  // workgroup -> (split, tile): XCD b % 8 owns splits [(b % 8) S/8, (b % 8 + 1) S/8)
+  const int b = blockIdx.x, per_xcd = S >> 3, i = b >> 3;
+  const int split = (b & 7) * per_xcd + i % per_xcd, tile = i / per_xcd, mt = M / kWgM;
+  const int m0 = (tile % mt) * kWgM, n0 = (tile / mt) * kWgN;
+  const int64_t rb = (int64_t)split * rows_per_split;
+  const int64_t re = min(rb + rows_per_split, R);
+  const int nch = re > rb ? (int)((re - rb + kWgR - 1) / kWgR) : 0;
+  // load tasks: A (column t & 63, row group t >> 6), B (column t & 127, row groups t >> 7 and + 2).  Raw buffer
+  // loads over the range's rows: the row offset is a wave-uniform SGPR operand, the lane's column offset a
+  // constant VGPR, and rows at or past the range's end lie outside the descriptor's records and read as zero.
+  const int am = t & 63, bn = t & 127;
+  const int ag = __builtin_amdgcn_readfirstlane(t >> 6), bg = __builtin_amdgcn_readfirstlane(t >> 7);
+  const int rows_here = re > rb ? (int)(re - rb) : 0;
+  const int a_ld4 = (int)(dy_ld * 4), b_ld4 = (int)(x_ld * 4);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy + rb * dy_ld), (short)0,
+                                                                     rows_here * a_ld4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + rb * x_ld), (short)0,
+                                                                      rows_here * b_ld4, 0x00020000);
+  const int va_off = (m0 + am) * 4, vb_off = (n0 + bn) * 4;
+  auto load = [&](int c, WgradRegs& v) {
+    const int ra0 = (c * kWgR + 8 * ag) * a_ld4;
+    const int rb0 = (c * kWgR + 8 * bg) * b_ld4;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v.a[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, va_off, ra0 + k * a_ld4, 0));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        v.b[h][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbx, vb_off, rb0 + (16 * h + k) * b_ld4, 0));
+    }
+  };
+  auto store = [&](int buf, const WgradRegs& v) {
+    u32x4_t hi, mi, lo;
+    split_bf16x3(make_float4(v.a[0], v.a[1], v.a[2], v.a[3]), make_float4(v.a[4], v.a[5], v.a[6], v.a[7]), hi, mi, lo);
+    const int qa = wgrad_quad(am, ag);
+    reinterpret_cast<u32x4_t*>(la[buf][0])[qa] = hi;
+    reinterpret_cast<u32x4_t*>(la[buf][1])[qa] = mi;
+    reinterpret_cast<u32x4_t*>(la[buf][2])[qa] = lo;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      split_bf16x3(make_float4(v.b[h][0], v.b[h][1], v.b[h][2], v.b[h][3]),
+                   make_float4(v.b[h][4], v.b[h][5], v.b[h][6], v.b[h][7]), hi, mi, lo);
+      const int qb = wgrad_quad(bn, bg + 2 * h);
+      reinterpret_cast<u32x4_t*>(lb[buf][0])[qb] = hi;
+      reinterpret_cast<u32x4_t*>(lb[buf][1])[qb] = mi;
+      reinterpret_cast<u32x4_t*>(lb[buf][2])[qb] = lo;
+    }
+  };
+  f32x4_t acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int buf) {
+    // A fragment: row (m) 16 w + l16, k = 8 q .. + 7; B fragment of n-tile j: column 16 j + l16
+    const int qa = wgrad_quad(16 * w + l16, q);
+    const u32x4_t ah = reinterpret_cast<const u32x4_t*>(la[buf][0])[qa];
+    const u32x4_t am_ = reinterpret_cast<const u32x4_t*>(la[buf][1])[qa];
+    const u32x4_t al = reinterpret_cast<const u32x4_t*>(la[buf][2])[qa];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int qb = wgrad_quad(16 * j + l16, q);
+      const u32x4_t bh = reinterpret_cast<const u32x4_t*>(lb[buf][0])[qb];
+      const u32x4_t bm = reinterpret_cast<const u32x4_t*>(lb[buf][1])[qb];
+      const u32x4_t bl = reinterpret_cast<const u32x4_t*>(lb[buf][2])[qb];
+      f32x4_t a = acc[j];  // small terms first
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_), as_bf16x8(bm), a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(al), as_bf16x8(bh), a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bl), a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_), as_bf16x8(bh), a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bm), a, 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bh), a, 0, 0, 0);
+    }
+  };
+  // chunk k's loads land in register set k & 1; iteration c: MFMAs on buffer c & 1, chunk c + 1 into the other
+  // buffer, then chunk c + 3's loads into the set chunk c + 1 has left
+  WgradRegs r0, r1;
+  if (nch > 0) {
+    load(0, r0);
+    store(0, r0);
+    if (nch > 1) load(1, r1);
+    if (nch > 2) load(2, r0);
+  }
+  __syncthreads();
+  auto step = [&](int c, WgradRegs& nxt) {
+    mma(c & 1);
+    if (c + 1 < nch) store((c + 1) & 1, nxt);
+    if (c + 3 < nch) load(c + 3, nxt);
+    __syncthreads();
+  };
+  for (int c = 0; c < nch; c += 2) {
+    step(c, r1);
+    if (c + 1 < nch) step(c + 1, r0);
+  }
+  // acc[j][e]: m = m0 + 16 w + 4 q + e, n = n0 + 16 j + l16
+  float* pp = part + (int64_t)split * M * N;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pp[(int64_t)(m0 + 16 * w + 4 * q + e) * N + n0 + 16 * j + l16] = acc[j][e];
+}
+
+// dW = the S partials summed in range order, written with row stride dw_ld (float4 per thread)
+__global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                        float* __restrict__ dw, int64_t dw_ld) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total4 = (int64_t)M * N / 4;
+  if (i4 >= total4) return;
+  float4 a = reinterpret_cast<const float4*>(part)[i4];
+  for (int s = 1; s < S; ++s) {
+    const float4 b = reinterpret_cast<const float4*>(part + (int64_t)s * M * N)[i4];
+    a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  const int64_t m = (4 * i4) / N, n = 4 * i4 - m * N;
+  *reinterpret_cast<float4*>(dw + m * dw_ld + n) = a;
+}
+
+static int wgrad_splits(int64_t rows, int M, int N) {
+  // a multiple of 8 (one slice of row ranges per XCD), >= 512 workgroups, a whole number of 512-workgroup
+  // waves (2 per CU) where doubling gets there; at least one chunk per range
+  (void)rows;
+  const int64_t tiles = (int64_t)(M / kWgM) * (N / kWgN);
+  int64_t k = std::max<int64_t>(1, (64 + tiles - 1) / tiles);
+  if ((tiles * 8 * k) % 512 && (tiles * 16 * k) % 512 == 0) k *= 2;
+  return (int)std::min<int64_t>(8 * k, 64);
+}
+
 // The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
 // caller buffer): the GEMM that follows runs at a padded width hipBLASLt is fast at (28-30 us for 192
 // outputs against 38-39 us for the 166 of decoder.py:87-88 at config 2).  One launch, fresh every call.
@@ -1131,6 +1280,46 @@ int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, cons
   const dim3 grid((unsigned)((rows + kMlpRows - 1) / kMlpRows), (unsigned)((n1 + n2 + kProjCols - 1) / kProjCols));
   hipLaunchKernelGGL(proj_bf3_sk_kernel, grid, dim3(512), 0, reinterpret_cast<hipStream_t>(stream), x, x_ld, w1, w1_ld, b1,
                      (int)n1, w2, w2_ld, b2, (int)n2, y, y_ld, rows);
+  return launch_status();
+}
+
+size_t ddsp_hip_linear_weight_grad_workspace_size(int64_t rows, int64_t out_features, int64_t in_features) {
+  if (rows < 1 || out_features < 1 || in_features < 1 || out_features > INT32_MAX || in_features > INT32_MAX) return 0;
+  return sizeof(float) * (size_t)wgrad_splits(rows, (int)out_features, (int)in_features) * (size_t)out_features *
+         (size_t)in_features;
+}
+
+int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float* x, int64_t x_ld, float* grad_w,
+                                int64_t dw_ld, int64_t rows, int64_t out_features, int64_t in_features, void* ws,
+                                size_t ws_bytes, void* stream) {
+  if (rows < 0 || out_features < 1 || in_features < 1) return DDSP_HIP_EINVAL;
+  if (!grad_w || dw_ld < in_features) return DDSP_HIP_EINVAL;
+  if (rows > 0 && (!grad_y || !x || dy_ld < out_features || x_ld < in_features)) return DDSP_HIP_EINVAL;
+  if (out_features % kWgM || in_features % kWgN || (dw_ld & 3) || (reinterpret_cast<uintptr_t>(grad_w) & 15) ||
+      out_features / kWgM > 65535 || in_features / kWgN > 65535)
+    return DDSP_HIP_ERANGE;  // callers keep their library GEMM
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    for (int64_t m = 0; m < out_features; ++m)
+      if (hipMemsetAsync(grad_w + m * dw_ld, 0, sizeof(float) * (size_t)in_features, st) != hipSuccess)
+        return DDSP_HIP_ELAUNCH;
+    return DDSP_HIP_OK;
+  }
+  const int M = (int)out_features, N = (int)in_features;
+  const int S = wgrad_splits(rows, M, N);
+  if (!ws || ws_bytes < ddsp_hip_linear_weight_grad_workspace_size(rows, out_features, in_features))
+    return DDSP_HIP_EWORKSPACE;
+  const int64_t chunks = (rows + kWgR - 1) / kWgR;
+  const int64_t per = ((chunks + S - 1) / S) * kWgR;  // rows per range (whole chunks; trailing ranges may be empty)
+  const int64_t tiles = (int64_t)(M / kWgM) * (N / kWgN);
+  if (tiles * S > INT32_MAX) return DDSP_HIP_ERANGE;
+  // 32-bit buffer offsets over one range (+ one chunk of rows past its end)
+  if ((per + kWgR) * std::max(dy_ld, x_ld) * 4 > INT32_MAX) return DDSP_HIP_ERANGE;
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(wgrad_bf3_kernel, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part, rows,
+                     M, N, S, per);
+  hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)(((int64_t)M * N / 4 + 255) / 256)), dim3(256), 0, st, part, S,
+                     M, N, grad_w, dw_ld);
   return launch_status();
 }
 

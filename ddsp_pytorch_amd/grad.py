@@ -436,7 +436,8 @@ class LinearFn(_F):
     """nn.Linear under autograd for the decoder's MLP blocks (ddsp/core.py:122-129, decoder.py:43-68): the
     forward and the input gradient on ddsp_hip_linear (core.linear: the bf16 matrix cores with the exact
     three-term split, fp32-accurate; torch.addmm outside its shapes) — y = x W^T + b and dx = dy W (the same
-    kernel over W^T) — the weight and bias gradients dW = dy^T x, db = sum dy on torch (hipBLASLt)."""
+    kernel over W^T) — and the weight gradient dW = dy^T x on ddsp_hip_linear_weight_grad (core.linear_weight_grad,
+    same split; torch.mm outside its shapes); db = sum dy on torch."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -456,7 +457,7 @@ class LinearFn(_F):
             wt = w.t().contiguous()
             gx = core.linear(g2, wt, torch.zeros(wt.shape[0], dtype=wt.dtype, device=wt.device)).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
-            gw = g2.t().mm(x2)
+            gw = core.linear_weight_grad(g2, x2)
         if ctx.needs_input_grad[2]:
             gb = g2.sum(0)
         return gx, gw, gb
@@ -499,8 +500,8 @@ class LNLeakyFn(_F):
 
 class GRUFn(_F):
     """decoder.py:33-68's nn.GRU (1 layer, batch_first) with BPTT on the gfx950 kernels (csrc/gru.hip); the input
-    projection and its input gradient on the matrix-core linear kernel (core.linear), the weight gradients
-    plain GEMMs."""
+    projection and its input gradient on the matrix-core linear kernel (core.linear), the weight gradients on
+    its weight-gradient kernel (core.linear_weight_grad)."""
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, h0):
@@ -546,8 +547,8 @@ class GRUFn(_F):
         if ctx.needs_input_grad[0]:  # dx = dxp W_ih on the matrix-core kernel (W_ih^T as its weight; addmm outside it)
             wt = w_ih.t().contiguous()
             dx = core.linear(dxp2, wt, torch.zeros(wt.shape[0], dtype=wt.dtype, device=wt.device)).view(B, T, I)
-        dw_ih = dxp2.t() @ x.reshape(B * T, I) if ctx.needs_input_grad[1] else None
-        dw_hh = dG.t() @ hprev if ctx.needs_input_grad[2] else None
+        dw_ih = core.linear_weight_grad(dxp2, x.reshape(B * T, I)) if ctx.needs_input_grad[1] else None
+        dw_hh = core.linear_weight_grad(dG, hprev) if ctx.needs_input_grad[2] else None
         db_ih = dxp2.sum(0) if ctx.needs_input_grad[3] else None
         db_hh = dG.sum(0) if ctx.needs_input_grad[4] else None
         dh0r = dh0.view(ctx.h0_shape) if (ctx.has_h0 and ctx.needs_input_grad[5]) else None

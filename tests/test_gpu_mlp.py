@@ -256,7 +256,7 @@ def test_projections_route_and_envelope(dd, monkeypatch):
 @pytest.mark.parametrize("rows,K,N", [(12800, 512, 512), (300, 1024, 512), (77, 514, 512)])
 def test_linear_fn_autograd(dd, rows, K, N):
     """grad.LinearFn (the decoder's MLP Linears under autograd: forward and input gradient on ddsp_hip_linear,
-    weight / bias gradients on torch) against an fp64 evaluation: output and all three gradients within 2x
+    the weight gradient on ddsp_hip_linear_weight_grad, the bias gradient on torch) against an fp64 evaluation: output and all three gradients within 2x
     of torch's fp32 Linear's error.  K = 514 (the out_mlp's first block) runs torch's GEMMs inside it."""
     from ddsp_pytorch_amd.grad import LinearFn
     torch.manual_seed(rows + K)
@@ -279,6 +279,52 @@ def test_linear_fn_autograd(dd, rows, K, N):
         assert rms(ours.double() - r) <= 2 * rms(f32.double() - r) + 1e-12, (rms(ours.double() - r), rms(f32.double() - r))
 
 
+@pytest.mark.parametrize("rows,M,N", [(12800, 512, 512), (12800, 1536, 1024), (12800, 1536, 512), (33, 512, 512),
+                                      (1, 64, 128), (5001, 192, 256), (100, 166, 512)])
+def test_linear_weight_grad_bf16x3(dd, rows, M, N):
+    """core.linear_weight_grad (ddsp_hip_linear_weight_grad: dW = dy^T x of the decoder's MLP Linears and the
+    GRU's W_ih / W_hh under autograd) against an fp64 evaluation: within 2x of the f32 GEMM's (torch.mm) error,
+    RMS and (3x) max; ragged row counts (33, 1, 5001: a partial last chunk and uneven row ranges); 166 outputs
+    are outside the kernel and run torch.mm.  Two calls are bit-identical (the row-range partials are summed in
+    a fixed order)."""
+    torch.manual_seed(rows + M + N)
+    gy = torch.randn(rows, M, device="cuda")
+    x = torch.randn(rows, N, device="cuda") * 1.5
+    with torch.no_grad():
+        dw = dd.core.linear_weight_grad(gy, x)
+        dw2 = dd.core.linear_weight_grad(gy, x)
+        d32 = gy.t().mm(x)
+        ref = gy.double().t() @ x.double()
+    assert dw.shape == (M, N)
+    assert torch.equal(dw, dw2)
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    # + one fp32 rounding of the result: at one row the f32 GEMM is a single rounded product, the split's
+    # dropped low-order terms (~2^-24 relative) then dominate the comparison
+    ulp = 2.0 ** -24
+    assert rms(dw.double() - ref) <= 2 * rms(d32.double() - ref) + ulp * rms(ref), (rms(dw.double() - ref), rms(d32.double() - ref))
+    assert float((dw.double() - ref).abs().max()) <= 3 * float((d32.double() - ref).abs().max()) + ulp * float(ref.abs().max())
+
+
+def test_linear_weight_grad_strides(dd):
+    """ddsp_hip_linear_weight_grad through the C-ABI with row strides past the columns (dy_ld, x_ld, dw_ld) and
+    zero rows (dW = 0): the strided result equals the packed one bit for bit; the padding of dW is untouched."""
+    from ddsp_pytorch_amd import _lib
+    torch.manual_seed(5)
+    rows, M, N = 3000, 128, 256
+    gyb = torch.randn(rows, M + 7, device="cuda")
+    xb = torch.randn(rows, N + 5, device="cuda")
+    dwb = torch.full((M, N + 4), 7.0, device="cuda")
+    ws = dd.core._workspace(_lib.query("linear_weight_grad_workspace_size", rows, M, N), xb.device)
+    _lib.call("linear_weight_grad", _lib.ptr(gyb), M + 7, _lib.ptr(xb), N + 5, _lib.ptr(dwb), N + 4, rows, M, N,
+              _lib.ptr(ws), ws.numel(), _lib.stream_of(dwb))
+    packed = dd.core.linear_weight_grad(gyb[:, :M].contiguous(), xb[:, :N].contiguous())
+    assert torch.equal(dwb[:, :N], packed)
+    assert bool((dwb[:, N:] == 7.0).all())
+    _lib.call("linear_weight_grad", _lib.ptr(gyb), M + 7, _lib.ptr(xb), N + 5, _lib.ptr(dwb), N + 4, 0, M, N,
+              _lib.ptr(ws), ws.numel(), _lib.stream_of(dwb))
+    assert bool((dwb[:, :N] == 0).all()) and bool((dwb[:, N:] == 7.0).all())
+
+
 def test_mlp_autograd_route(dd, monkeypatch):
     """Under autograd the decoder's MLPs (mlp_forward) run each block's Linear on LinearFn — the 512-input blocks'
     forward and input gradient on the matrix-core kernel — and match torch's modules (values and every
@@ -295,6 +341,7 @@ def test_mlp_autograd_route(dd, monkeypatch):
     y.pow(2).mean().backward()
     ours = [p.grad.clone() for p in seq.parameters()]
     assert calls.count("linear") == 4, calls  # blocks 2 and 3: forward + input gradient each
+    assert calls.count("linear_weight_grad") == 2, calls  # and their weight gradients
     assert calls.count("layer_norm_leaky_relu") == 3 and calls.count("layer_norm_leaky_relu_backward") == 3, calls
     seq.zero_grad()
     y_ref = seq(x)
