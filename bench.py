@@ -341,8 +341,9 @@ def loss_leg(args, dev, reps=10):
 def model_train_leg(args, inp, dev, reps=5):
     """train.py:84-130's step at config 2's shape: DDSPDecoder.forward (hidden 512) -> fused spectral
     loss -> backward -> Adam step, all gradients on the gfx950 kernels (synthesis VJPs, GRU BPTT,
-    STFT loss).  The network's MLPs/GEMMs are hipBLASLt through torch.  Random-init weights and a
-    synthetic target signal."""
+    STFT loss, the MLP blocks' Linear / LayerNorm + LeakyReLU forward and backward, the Linears' and the
+    GRU's weight gradients; the one-feature first Linears, the 514-input out_mlp block and the output
+    projections stay on torch under autograd).  Random-init weights and a synthetic target signal."""
     from ddsp_pytorch_amd.decoder import DDSPDecoder
     from ddsp_pytorch_amd.loss import spectral_loss
     B, F, bs = args.batch, args.frames, args.block_size
