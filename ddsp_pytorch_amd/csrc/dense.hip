@@ -949,32 +949,52 @@ __global__ void __launch_bounds__(512) proj_bf3_sk_kernel(
 // under the current chunk's 48 MFMAs per wave (wave w: m-tile w x the 8 n-tiles).  Row ranges are sliced by XCD
 // (S a multiple of 8, workgroup b on XCD b % 8 takes ranges of slice b % 8): an XCD streams only its eighth of
 // dY and X from HBM and serves the tiles' re-reads from its own L2.
-constexpr int kWgM = 64, kWgN = 128, kWgR = 32, kWgBufs = 1;
-__device__ __forceinline__ int wgrad_quad(int col, int q) { return col * (kWgR / 8) + (q ^ ((0x78 >> (2 * ((col >> 2) & 3))) & 3)); }
-struct WgradRegs {
-  float a[8], b[2][8];
-};
+constexpr int kWgN = 128, kWgR = 32, kWgBufs = 1;
+// LDS quad of [column][row group q]: the group index XOR-swizzled by column bits 1..3 so that both the fragment
+// reads (16-lane groups of 16 columns x 4 row groups) and the 16-byte stores (8-lane groups of 8 columns) are
+// conflict-free
+__device__ __forceinline__ int wgrad_quad(int col, int q) {
+  return col * (kWgR / 8) + (q ^ ((0x78 >> (2 * ((col >> 2) & 3))) & 3) ^ ((col >> 1) & 1));
+}
+// split_bf16x3 with the two exact residual subtractions on packed fp32 (v_pk_add_f32): the same bits
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wgrad_split(const float* v, u32x4_t& hi, u32x4_t& mid, u32x4_t& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t u0 = __float_as_uint(v[2 * e]), u1 = __float_as_uint(v[2 * e + 1]);
+    const f32x2v_t x = {v[2 * e], v[2 * e + 1]};
+    const f32x2v_t h = {__uint_as_float(u0 & 0xffff0000u), __uint_as_float(u1 & 0xffff0000u)};
+    const f32x2v_t r = x - h;  // exact
+    const uint32_t m0 = __float_as_uint(r.x) & 0xffff0000u, m1 = __float_as_uint(r.y) & 0xffff0000u;
+    const f32x2v_t l = r - (f32x2v_t){__uint_as_float(m0), __uint_as_float(m1)};  // exact
+    hi[e] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    mid[e] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+    lo[e] = __builtin_amdgcn_perm(__float_as_uint(l.y), __float_as_uint(l.x), 0x07060302u);
+  }
+}
+template <int WM>  // m-tiles per wave: the workgroup's dW tile is 64 WM x 128
 __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict__ dy, int64_t dy_ld,
                                                         const float* __restrict__ x, int64_t x_ld,
                                                         float* __restrict__ part, int64_t R, int M, int N, int S,
                                                         int64_t rows_per_split) {
-  // [buffer][plane][column][32 rows] bf16: A (dY) 64 columns, B (X) 128 columns
-  __shared__ __attribute__((aligned(16))) uint32_t la[kWgBufs][3][kWgM * kWgR / 2];
+  constexpr int TM = 64 * WM;
+  // [buffer][plane][column][32 rows] bf16: A (dY) TM columns, B (X) 128 columns
+  __shared__ __attribute__((aligned(16))) uint32_t la[kWgBufs][3][TM * kWgR / 2];
   __shared__ __attribute__((aligned(16))) uint32_t lb[kWgBufs][3][kWgN * kWgR / 2];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int q = lane >> 4, l16 = lane & 15;
   // workgroup -> (split, tile): XCD b % 8 owns splits [(b % 8) S/8, (b % 8 + 1) S/8)
   const int b = blockIdx.x, per_xcd = S >> 3, i = b >> 3;
-  const int split = (b & 7) * per_xcd + i % per_xcd, tile = i / per_xcd, mt = M / kWgM;
-  const int m0 = (tile % mt) * kWgM, n0 = (tile / mt) * kWgN;
+  const int split = (b & 7) * per_xcd + i % per_xcd, tile = i / per_xcd, mt = M / TM;
+  const int m0 = (tile % mt) * TM, n0 = (tile / mt) * kWgN;
   const int64_t rb = (int64_t)split * rows_per_split;
   const int64_t re = min(rb + rows_per_split, R);
   const int nch = re > rb ? (int)((re - rb + kWgR - 1) / kWgR) : 0;
-  // load tasks: A (column t & 63, row group t >> 6), B (column t & 127, row groups t >> 7 and + 2).  Raw buffer
-  // loads over the range's rows: the row offset is a wave-uniform SGPR operand, the lane's column offset a
-  // constant VGPR, and rows at or past the range's end lie outside the descriptor's records and read as zero.
-  const int am = t & 63, bn = t & 127;
-  const int ag = __builtin_amdgcn_readfirstlane(t >> 6), bg = __builtin_amdgcn_readfirstlane(t >> 7);
+  // load tasks: A column t % TM, row groups t / TM + (4 / WM) h (h < WM); B column t & 127, row groups t >> 7 and
+  // + 2.  Raw buffer loads over the range's rows: the row offset is a wave-uniform SGPR operand, the lane's column
+  // offset a constant VGPR, and rows at or past the range's end lie outside the descriptor's records and read 0.
+  const int am = t & (TM - 1), bn = t & 127;
+  const int ag = __builtin_amdgcn_readfirstlane(t / TM), bg = __builtin_amdgcn_readfirstlane(t >> 7);
   const int rows_here = re > rb ? (int)(re - rb) : 0;
   const int a_ld4 = (int)(dy_ld * 4), b_ld4 = (int)(x_ld * 4);
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy + rb * dy_ld), (short)0,
@@ -982,61 +1002,77 @@ __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict_
   const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + rb * x_ld), (short)0,
                                                                       rows_here * b_ld4, 0x00020000);
   const int va_off = (m0 + am) * 4, vb_off = (n0 + bn) * 4;
-  auto load = [&](int c, WgradRegs& v) {
+  struct Regs {
+    float a[WM][8], b[2][8];
+  };
+  auto load = [&](int c, Regs& v) {
     const int ra0 = (c * kWgR + 8 * ag) * a_ld4;
     const int rb0 = (c * kWgR + 8 * bg) * b_ld4;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      v.a[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, va_off, ra0 + k * a_ld4, 0));
+#pragma unroll
+      for (int h = 0; h < WM; ++h)
+        v.a[h][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, va_off, ra0 + (32 / WM * h + k) * a_ld4, 0));
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         v.b[h][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbx, vb_off, rb0 + (16 * h + k) * b_ld4, 0));
     }
   };
-  auto store = [&](int buf, const WgradRegs& v) {
+  auto store = [&](int buf, const Regs& v) {
     u32x4_t hi, mi, lo;
-    split_bf16x3(make_float4(v.a[0], v.a[1], v.a[2], v.a[3]), make_float4(v.a[4], v.a[5], v.a[6], v.a[7]), hi, mi, lo);
-    const int qa = wgrad_quad(am, ag);
-    reinterpret_cast<u32x4_t*>(la[buf][0])[qa] = hi;
-    reinterpret_cast<u32x4_t*>(la[buf][1])[qa] = mi;
-    reinterpret_cast<u32x4_t*>(la[buf][2])[qa] = lo;
+#pragma unroll
+    for (int h = 0; h < WM; ++h) {
+      wgrad_split(v.a[h], hi, mi, lo);
+      const int qa = wgrad_quad(am, ag + 4 / WM * h);
+      reinterpret_cast<u32x4_t*>(la[buf][0])[qa] = hi;
+      reinterpret_cast<u32x4_t*>(la[buf][1])[qa] = mi;
+      reinterpret_cast<u32x4_t*>(la[buf][2])[qa] = lo;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      split_bf16x3(make_float4(v.b[h][0], v.b[h][1], v.b[h][2], v.b[h][3]),
-                   make_float4(v.b[h][4], v.b[h][5], v.b[h][6], v.b[h][7]), hi, mi, lo);
+      wgrad_split(v.b[h], hi, mi, lo);
       const int qb = wgrad_quad(bn, bg + 2 * h);
       reinterpret_cast<u32x4_t*>(lb[buf][0])[qb] = hi;
       reinterpret_cast<u32x4_t*>(lb[buf][1])[qb] = mi;
       reinterpret_cast<u32x4_t*>(lb[buf][2])[qb] = lo;
     }
   };
-  f32x4_t acc[8];
+  f32x4_t acc[WM][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < WM; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[u][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   auto mma = [&](int buf) {
-    // A fragment: row (m) 16 w + l16, k = 8 q .. + 7; B fragment of n-tile j: column 16 j + l16
-    const int qa = wgrad_quad(16 * w + l16, q);
-    const u32x4_t ah = reinterpret_cast<const u32x4_t*>(la[buf][0])[qa];
-    const u32x4_t am_ = reinterpret_cast<const u32x4_t*>(la[buf][1])[qa];
-    const u32x4_t al = reinterpret_cast<const u32x4_t*>(la[buf][2])[qa];
+    // A fragment of m-tile u: row (m) 16 (WM w + u) + l16, k = 8 q .. + 7; B fragment of n-tile j: column 16 j + l16
+    u32x4_t ah[WM], am_[WM], al[WM];
+#pragma unroll
+    for (int u = 0; u < WM; ++u) {
+      const int qa = wgrad_quad(16 * (WM * w + u) + l16, q);
+      ah[u] = reinterpret_cast<const u32x4_t*>(la[buf][0])[qa];
+      am_[u] = reinterpret_cast<const u32x4_t*>(la[buf][1])[qa];
+      al[u] = reinterpret_cast<const u32x4_t*>(la[buf][2])[qa];
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int qb = wgrad_quad(16 * j + l16, q);
       const u32x4_t bh = reinterpret_cast<const u32x4_t*>(lb[buf][0])[qb];
       const u32x4_t bm = reinterpret_cast<const u32x4_t*>(lb[buf][1])[qb];
       const u32x4_t bl = reinterpret_cast<const u32x4_t*>(lb[buf][2])[qb];
-      f32x4_t a = acc[j];  // small terms first
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_), as_bf16x8(bm), a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(al), as_bf16x8(bh), a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bl), a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_), as_bf16x8(bh), a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bm), a, 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah), as_bf16x8(bh), a, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < WM; ++u) {
+        f32x4_t a = acc[u][j];  // small terms first
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_[u]), as_bf16x8(bm), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(al[u]), as_bf16x8(bh), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah[u]), as_bf16x8(bl), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(am_[u]), as_bf16x8(bh), a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah[u]), as_bf16x8(bm), a, 0, 0, 0);
+        acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ah[u]), as_bf16x8(bh), a, 0, 0, 0);
+      }
     }
   };
-  // chunk k's loads land in register set k & 1; iteration c: MFMAs on buffer c & 1, chunk c + 1 into the other
-  // buffer, then chunk c + 3's loads into the set chunk c + 1 has left
-  WgradRegs r0, r1;
+  // chunk k's loads land in register set k & 1; iteration c: MFMAs on the LDS tile, chunk c + 1 into LDS behind a
+  // barrier, then chunk c + 3's loads into the set chunk c + 1 has left
+  Regs r0, r1;
   if (nch > 0) {
     load(0, r0);
     store(0, r0);
@@ -1044,7 +1080,7 @@ __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict_
     if (nch > 2) load(2, r0);
   }
   __syncthreads();
-  auto step = [&](int c, WgradRegs& nxt) {
+  auto step = [&](int c, Regs& nxt) {
     mma(c & (kWgBufs - 1));
     if (kWgBufs == 1) __syncthreads();
     if (c + 1 < nch) store((c + 1) & (kWgBufs - 1), nxt);
@@ -1055,12 +1091,15 @@ __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict_
     step(c, r1);
     if (c + 1 < nch) step(c + 1, r0);
   }
-  // acc[j][e]: m = m0 + 16 w + 4 q + e, n = n0 + 16 j + l16
+  // acc[u][j][e]: m = m0 + 16 (WM w + u) + 4 q + e, n = n0 + 16 j + l16
   float* pp = part + (int64_t)split * M * N;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int u = 0; u < WM; ++u)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) pp[(int64_t)(m0 + 16 * w + 4 * q + e) * N + n0 + 16 * j + l16] = acc[j][e];
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        pp[(int64_t)(m0 + 16 * (WM * w + u) + 4 * q + e) * N + n0 + 16 * j + l16] = acc[u][j][e];
 }
 
 // dW = the S partials summed in range order, written with row stride dw_ld (float4 per thread)
@@ -1078,13 +1117,23 @@ __global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict_
   *reinterpret_cast<float4*>(dw + m * dw_ld + n) = a;
 }
 
-static int wgrad_splits(int64_t rows, int M, int N) {
-  // a multiple of 8 (one slice of row ranges per XCD) giving >= 512 workgroups (2 per CU; more ranges cost
-  // more partial traffic than the extra occupancy returns: 512 x 512 at 1024 workgroups measured 70 us, at 512 61 us)
-  (void)rows;
-  const int64_t tiles = (int64_t)(M / kWgM) * (N / kWgN);
+static int wgrad_splits_for(int64_t tiles) {
+  // a multiple of 8 (one slice of row ranges per XCD) giving >= 512 workgroups (more ranges cost more partial
+  // traffic than the extra occupancy returns: 512 x 512 at 1024 workgroups measured 70 us, at 512 61 us)
   const int64_t k = std::max<int64_t>(1, (64 + tiles - 1) / tiles);
   return (int)std::min<int64_t>(8 * k, 64);
+}
+// m-tiles per wave: 128-row dW tiles (twice the MFMAs per split element, 2 waves per SIMD) where they divide M and
+// fill whole 512-workgroup rounds, else 64-row tiles (4 waves per SIMD).  Same box, us (profiles/r06w_weight_grad.log):
+// 512 x 512 60 vs 64, W_ih 1536 x 1024 288 vs 270 (768 workgroups = 1.5 rounds), W_hh 1536 x 512 131 vs 129.
+static int wgrad_wm(int M, int N) {
+  if (M % 128) return 1;
+  const int64_t tiles = (int64_t)(M / 128) * (N / kWgN);
+  return (tiles * wgrad_splits_for(tiles)) % 512 == 0 ? 2 : 1;
+}
+static int wgrad_splits(int64_t rows, int M, int N) {
+  (void)rows;
+  return wgrad_splits_for((int64_t)(M / (64 * wgrad_wm(M, N))) * (N / kWgN));
 }
 
 // The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
@@ -1295,8 +1344,8 @@ int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float*
   if (rows < 0 || out_features < 1 || in_features < 1) return DDSP_HIP_EINVAL;
   if (!grad_w || dw_ld < in_features) return DDSP_HIP_EINVAL;
   if (rows > 0 && (!grad_y || !x || dy_ld < out_features || x_ld < in_features)) return DDSP_HIP_EINVAL;
-  if (out_features % kWgM || in_features % kWgN || (dw_ld & 3) || (reinterpret_cast<uintptr_t>(grad_w) & 15) ||
-      out_features / kWgM > 65535 || in_features / kWgN > 65535)
+  if (out_features % 64 || in_features % kWgN || (dw_ld & 3) || (reinterpret_cast<uintptr_t>(grad_w) & 15) ||
+      out_features / 64 > 65535 || in_features / kWgN > 65535)
     return DDSP_HIP_ERANGE;  // callers keep their library GEMM
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (rows == 0) {
@@ -1311,13 +1360,18 @@ int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float*
     return DDSP_HIP_EWORKSPACE;
   const int64_t chunks = (rows + kWgR - 1) / kWgR;
   const int64_t per = ((chunks + S - 1) / S) * kWgR;  // rows per range (whole chunks; trailing ranges may be empty)
-  const int64_t tiles = (int64_t)(M / kWgM) * (N / kWgN);
+  const int WM = wgrad_wm(M, N);
+  const int64_t tiles = (int64_t)(M / (64 * WM)) * (N / kWgN);
   if (tiles * S > INT32_MAX) return DDSP_HIP_ERANGE;
   // 32-bit buffer offsets over one range (+ one chunk of rows past its end)
   if ((per + kWgR) * std::max(dy_ld, x_ld) * 4 > INT32_MAX) return DDSP_HIP_ERANGE;
   float* part = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(wgrad_bf3_kernel, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part, rows,
-                     M, N, S, per);
+  if (WM == 2)
+    hipLaunchKernelGGL(wgrad_bf3_kernel<2>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part,
+                       rows, M, N, S, per);
+  else
+    hipLaunchKernelGGL(wgrad_bf3_kernel<1>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part,
+                       rows, M, N, S, per);
   hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)(((int64_t)M * N / 4 + 255) / 256)), dim3(256), 0, st, part, S,
                      M, N, grad_w, dw_ld);
   return launch_status();
