@@ -643,14 +643,13 @@ def linear(x, weight, bias):
 def linear_weight_grad(grad_y, x):
     """grad_y [rows, out]^T @ x [rows, in] -> [out, in], a Linear's weight gradient (no autograd):
     ddsp_hip_linear_weight_grad — the bf16 matrix cores with the fp32-accurate three-term split, split over
-    row ranges summed in a fixed order — where it applies (out % 64 == 0, in % 128 == 0), else torch.mm."""
+    row ranges summed in a fixed order (any widths; torch.mm only past its 32-bit range offsets)."""
     _dev(grad_y, x)
     rows, M = grad_y.shape
     N = x.shape[1]
     gc, xc = _c(grad_y), _c(x)
     dw = torch.empty(M, N, dtype=torch.float32, device=x.device)
-    nbytes = _lib.query("linear_weight_grad_workspace_size", max(rows, 1), M, N) if M % 64 == 0 and N % 128 == 0 else 0
-    ws = _workspace(nbytes, x.device)
+    ws = _workspace(_lib.query("linear_weight_grad_workspace_size", max(rows, 1), M, N), x.device)
     st = _lib.call("linear_weight_grad", _lib.ptr(gc), M, _lib.ptr(xc), N, _lib.ptr(dw), N, rows, M, N,
                    _lib.ptr(ws), ws.numel(), _lib.stream_of(dw), allow=(ERANGE,))
     return grad_y.t().mm(x) if st == ERANGE else dw

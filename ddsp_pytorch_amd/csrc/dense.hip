@@ -976,7 +976,8 @@ template <int WM>  // m-tiles per wave: the workgroup's dW tile is 64 WM x 128
 __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict__ dy, int64_t dy_ld,
                                                         const float* __restrict__ x, int64_t x_ld,
                                                         float* __restrict__ part, int64_t R, int M, int N, int S,
-                                                        int64_t rows_per_split) {
+                                                        int64_t rows_per_split, int Mr, int Nr) {
+  // M, N: the partials' padded extents (multiples of the tile); Mr, Nr: dW's own (columns of dY and X)
   constexpr int TM = 64 * WM;
   // [buffer][plane][column][32 rows] bf16: A (dY) TM columns, B (X) 128 columns
   __shared__ __attribute__((aligned(16))) uint32_t la[kWgBufs][3][TM * kWgR / 2];
@@ -997,10 +998,12 @@ __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict_
   const int ag = __builtin_amdgcn_readfirstlane(t / TM), bg = __builtin_amdgcn_readfirstlane(t >> 7);
   const int rows_here = re > rb ? (int)(re - rb) : 0;
   const int a_ld4 = (int)(dy_ld * 4), b_ld4 = (int)(x_ld * 4);
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy + rb * dy_ld), (short)0,
-                                                                     rows_here * a_ld4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + rb * x_ld), (short)0,
-                                                                      rows_here * b_ld4, 0x00020000);
+  // records end at the range's last element: columns past dW's edge read the next row (their products land in
+  // the padding of the partials) or, on the last row, zero — never memory past the operands
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(dy + rb * dy_ld), (short)0, rows_here ? (rows_here - 1) * a_ld4 + 4 * Mr : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + rb * x_ld), (short)0, rows_here ? (rows_here - 1) * b_ld4 + 4 * Nr : 0, 0x00020000);
   const int va_off = (m0 + am) * 4, vb_off = (n0 + bn) * 4;
   struct Regs {
     float a[WM][8], b[2][8];
@@ -1102,19 +1105,26 @@ __global__ void __launch_bounds__(256) wgrad_bf3_kernel(const float* __restrict_
         pp[(int64_t)(m0 + 16 * (WM * w + u) + 4 * q + e) * N + n0 + 16 * j + l16] = acc[u][j][e];
 }
 
-// dW = the S partials summed in range order, written with row stride dw_ld (float4 per thread)
-__global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict__ part, int S, int M, int N,
-                                                        float* __restrict__ dw, int64_t dw_ld) {
+// dW = the S partials ([S][M][N] padded) summed in range order, written with row stride dw_ld: 4 columns per
+// thread, one 16-byte store where dW's row holds all four and is aligned, else element stores
+__global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict__ part, int S, int M, int N, int Mr,
+                                                        int Nr, float* __restrict__ dw, int64_t dw_ld, int vec) {
   const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total4 = (int64_t)M * N / 4;
-  if (i4 >= total4) return;
+  if (i4 >= (int64_t)Mr * N / 4) return;
+  const int64_t m = (4 * i4) / N, n = 4 * i4 - m * N;
+  if (n >= Nr) return;
   float4 a = reinterpret_cast<const float4*>(part)[i4];
   for (int s = 1; s < S; ++s) {
     const float4 b = reinterpret_cast<const float4*>(part + (int64_t)s * M * N)[i4];
     a = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
   }
-  const int64_t m = (4 * i4) / N, n = 4 * i4 - m * N;
-  *reinterpret_cast<float4*>(dw + m * dw_ld + n) = a;
+  float* o = dw + m * dw_ld + n;
+  if (vec && n + 4 <= Nr) {
+    *reinterpret_cast<float4*>(o) = a;
+  } else {
+    const float v[4] = {a.x, a.y, a.z, a.w};
+    for (int e = 0; e < 4 && n + e < Nr; ++e) o[e] = v[e];
+  }
 }
 
 static int wgrad_splits_for(int64_t tiles) {
@@ -1128,12 +1138,19 @@ static int wgrad_splits_for(int64_t tiles) {
 // 512 x 512 60 vs 64, W_ih 1536 x 1024 288 vs 270 (768 workgroups = 1.5 rounds), W_hh 1536 x 512 131 vs 129.
 static int wgrad_wm(int M, int N) {
   if (M % 128) return 1;
-  const int64_t tiles = (int64_t)(M / 128) * (N / kWgN);
+  const int64_t tiles = (int64_t)(M / 128) * ((N + kWgN - 1) / kWgN);
   return (tiles * wgrad_splits_for(tiles)) % 512 == 0 ? 2 : 1;
 }
-static int wgrad_splits(int64_t rows, int M, int N) {
-  (void)rows;
-  return wgrad_splits_for((int64_t)(M / (64 * wgrad_wm(M, N))) * (N / kWgN));
+struct WgradShape {
+  int wm, S, Mp, Np;  // tile height / 64, row ranges, padded extents of the partials
+};
+static WgradShape wgrad_shape(int M, int N) {
+  WgradShape g;
+  g.wm = wgrad_wm(M, N);
+  g.Mp = (M + 64 * g.wm - 1) / (64 * g.wm) * (64 * g.wm);
+  g.Np = (N + kWgN - 1) / kWgN * kWgN;
+  g.S = wgrad_splits_for((int64_t)(g.Mp / (64 * g.wm)) * (g.Np / kWgN));
+  return g;
 }
 
 // The two projections' parameters stacked into one zero-padded [n_pad, K] weight and [n_pad] bias (a
@@ -1333,9 +1350,9 @@ int ddsp_hip_projections(const float* x, int64_t x_ld, int64_t in_features, cons
 }
 
 size_t ddsp_hip_linear_weight_grad_workspace_size(int64_t rows, int64_t out_features, int64_t in_features) {
-  if (rows < 1 || out_features < 1 || in_features < 1 || out_features > INT32_MAX || in_features > INT32_MAX) return 0;
-  return sizeof(float) * (size_t)wgrad_splits(rows, (int)out_features, (int)in_features) * (size_t)out_features *
-         (size_t)in_features;
+  if (rows < 1 || out_features < 1 || in_features < 1 || out_features > (1 << 24) || in_features > (1 << 24)) return 0;
+  const WgradShape g = wgrad_shape((int)out_features, (int)in_features);
+  return sizeof(float) * (size_t)g.S * (size_t)g.Mp * (size_t)g.Np;
 }
 
 int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float* x, int64_t x_ld, float* grad_w,
@@ -1344,9 +1361,7 @@ int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float*
   if (rows < 0 || out_features < 1 || in_features < 1) return DDSP_HIP_EINVAL;
   if (!grad_w || dw_ld < in_features) return DDSP_HIP_EINVAL;
   if (rows > 0 && (!grad_y || !x || dy_ld < out_features || x_ld < in_features)) return DDSP_HIP_EINVAL;
-  if (out_features % 64 || in_features % kWgN || (dw_ld & 3) || (reinterpret_cast<uintptr_t>(grad_w) & 15) ||
-      out_features / 64 > 65535 || in_features / kWgN > 65535)
-    return DDSP_HIP_ERANGE;  // callers keep their library GEMM
+  if (out_features > (1 << 24) || in_features > (1 << 24)) return DDSP_HIP_ERANGE;  // callers keep their library GEMM
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (rows == 0) {
     for (int64_t m = 0; m < out_features; ++m)
@@ -1355,25 +1370,24 @@ int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float*
     return DDSP_HIP_OK;
   }
   const int M = (int)out_features, N = (int)in_features;
-  const int S = wgrad_splits(rows, M, N);
+  const WgradShape g = wgrad_shape(M, N);
+  const int64_t chunks = (rows + kWgR - 1) / kWgR;
+  const int64_t per = ((chunks + g.S - 1) / g.S) * kWgR;  // rows per range (whole chunks; trailing ranges may be empty)
+  const int64_t tiles = (int64_t)(g.Mp / (64 * g.wm)) * (g.Np / kWgN);
+  // the grid, and 32-bit buffer offsets over one range (+ one chunk of rows past its end)
+  if (tiles * g.S > INT32_MAX || (per + kWgR) * std::max(dy_ld, x_ld) * 4 > INT32_MAX) return DDSP_HIP_ERANGE;
   if (!ws || ws_bytes < ddsp_hip_linear_weight_grad_workspace_size(rows, out_features, in_features))
     return DDSP_HIP_EWORKSPACE;
-  const int64_t chunks = (rows + kWgR - 1) / kWgR;
-  const int64_t per = ((chunks + S - 1) / S) * kWgR;  // rows per range (whole chunks; trailing ranges may be empty)
-  const int WM = wgrad_wm(M, N);
-  const int64_t tiles = (int64_t)(M / (64 * WM)) * (N / kWgN);
-  if (tiles * S > INT32_MAX) return DDSP_HIP_ERANGE;
-  // 32-bit buffer offsets over one range (+ one chunk of rows past its end)
-  if ((per + kWgR) * std::max(dy_ld, x_ld) * 4 > INT32_MAX) return DDSP_HIP_ERANGE;
   float* part = reinterpret_cast<float*>(ws);
-  if (WM == 2)
-    hipLaunchKernelGGL(wgrad_bf3_kernel<2>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part,
-                       rows, M, N, S, per);
+  if (g.wm == 2)
+    hipLaunchKernelGGL(wgrad_bf3_kernel<2>, dim3((unsigned)(tiles * g.S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld,
+                       part, rows, g.Mp, g.Np, g.S, per, M, N);
   else
-    hipLaunchKernelGGL(wgrad_bf3_kernel<1>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld, part,
-                       rows, M, N, S, per);
-  hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)(((int64_t)M * N / 4 + 255) / 256)), dim3(256), 0, st, part, S,
-                     M, N, grad_w, dw_ld);
+    hipLaunchKernelGGL(wgrad_bf3_kernel<1>, dim3((unsigned)(tiles * g.S)), dim3(256), 0, st, grad_y, dy_ld, x, x_ld,
+                       part, rows, g.Mp, g.Np, g.S, per, M, N);
+  const int vec = !(dw_ld & 3) && !(reinterpret_cast<uintptr_t>(grad_w) & 15);
+  hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)(((int64_t)M * g.Np / 4 + 255) / 256)), dim3(256), 0, st, part,
+                     g.S, g.Mp, g.Np, M, N, grad_w, dw_ld, vec);
   return launch_status();
 }
 

@@ -130,11 +130,13 @@ def test_training_entry_points_reject_bad_arguments_without_launching():
                                     null) == ERANGE
     assert lib.ddsp_hip_projections(dummy, 512, 512, dummy, 512, dummy, 101, dummy, 512, dummy, 65, dummy, 168, 0,
                                     null) == 0
-    # a Linear's weight gradient: missing operands, shapes outside the kernel, a short workspace
+    # a Linear's weight gradient: missing operands, sizes outside the kernel (32-bit offsets over a row range),
+    # a short workspace (ragged widths are in range)
     assert lib.ddsp_hip_linear_weight_grad(null, 512, null, 512, null, 512, 10, 512, 512, null, 0, null) == EINVAL
     assert lib.ddsp_hip_linear_weight_grad(dummy, 512, dummy, 512, dummy, 500, 10, 512, 512, null, 0, null) == EINVAL
-    assert lib.ddsp_hip_linear_weight_grad(dummy, 166, dummy, 512, dummy, 512, 10, 166, 512, null, 0, null) == ERANGE
-    assert lib.ddsp_hip_linear_weight_grad(dummy, 512, dummy, 514, dummy, 516, 10, 512, 514, null, 0, null) == ERANGE
+    assert lib.ddsp_hip_linear_weight_grad(dummy, 1 << 27, dummy, 512, dummy, 512, 10, 512, 512, null, 0, null) == ERANGE
+    assert lib.ddsp_hip_linear_weight_grad(dummy, 166, dummy, 512, dummy, 512, 10, 166, 512, null, 0, null) == EWS
+    assert lib.ddsp_hip_linear_weight_grad(dummy, 512, dummy, 514, dummy, 514, 10, 512, 514, null, 0, null) == EWS
     assert lib.ddsp_hip_linear_weight_grad(dummy, 512, dummy, 512, dummy, 512, 10, 512, 512, null, 0, null) == EWS
     assert lib.ddsp_hip_linear_weight_grad_workspace_size(12800, 512, 512) >= 4 * 512 * 512
     assert lib.ddsp_hip_linear_weight_grad_workspace_size(0, 512, 512) == 0

@@ -280,13 +280,14 @@ def test_linear_fn_autograd(dd, rows, K, N):
 
 
 @pytest.mark.parametrize("rows,M,N", [(12800, 512, 512), (12800, 1536, 1024), (12800, 1536, 512), (33, 512, 512),
-                                      (1, 64, 128), (5001, 192, 256), (100, 166, 512)])
+                                      (1, 64, 128), (5001, 192, 256), (100, 166, 512), (12800, 101, 512),
+                                      (12800, 65, 512), (12800, 512, 514), (37, 3, 5)])
 def test_linear_weight_grad_bf16x3(dd, rows, M, N):
     """core.linear_weight_grad (ddsp_hip_linear_weight_grad: dW = dy^T x of the decoder's MLP Linears and the
     GRU's W_ih / W_hh under autograd) against an fp64 evaluation: within 2x of the f32 GEMM's (torch.mm) error,
-    RMS and (3x) max; ragged row counts (33, 1, 5001: a partial last chunk and uneven row ranges); 166 outputs
-    are outside the kernel and run torch.mm.  Two calls are bit-identical (the row-range partials are summed in
-    a fixed order)."""
+    RMS and (3x) max; ragged row counts (33, 1, 5001: a partial last chunk and uneven row ranges) and widths that
+    are no multiple of the tile (the decoder's 101 / 65-output projections, the out_mlp's 514 inputs, 3 x 5).
+    Two calls are bit-identical (the row-range partials are summed in a fixed order)."""
     torch.manual_seed(rows + M + N)
     gy = torch.randn(rows, M, device="cuda")
     x = torch.randn(rows, N, device="cuda") * 1.5
