@@ -285,11 +285,12 @@ int ddsp_hip_layer_norm_leaky_relu(const float* x, int64_t x_ld, const float* w1
 
 /* Weight gradient of a Linear under autograd, grad_w[m][n] = sum_r grad_y[r][m] x[r][n] (grad_w [out_features,
  * dw_ld], nn.Linear's weight layout; torch: grad_y^T @ x), on the bf16 matrix cores with the fp32-accurate
- * three-term split: the decoder MLPs' Linears (core.py:122-129) and the GRU's W_ih / W_hh (decoder.py:33-68).
- * Split over row ranges whose partials are summed in a fixed order (deterministic).  ws:
- * ddsp_hip_linear_weight_grad_workspace_size(rows, out_features, in_features) bytes.  out_features % 64 == 0,
- * in_features % 128 == 0, grad_w 16-byte aligned with dw_ld % 4 == 0; else DDSP_HIP_ERANGE (callers keep their
- * library GEMM). */
+ * three-term split: the decoder MLPs' Linears and projections (core.py:122-129, decoder.py:106-117) and the GRU's
+ * W_ih / W_hh (decoder.py:33-68).  Any widths (tiles past an edge are padding of the partials); split over row
+ * ranges whose partials are summed in a fixed order (deterministic).  ws:
+ * ddsp_hip_linear_weight_grad_workspace_size(rows, out_features, in_features) bytes.  DDSP_HIP_ERANGE when a row
+ * range's byte offsets pass 2^31 (dy_ld / x_ld beyond ~2^24 floats) or a width passes 2^24: callers keep their
+ * library GEMM. */
 size_t ddsp_hip_linear_weight_grad_workspace_size(int64_t rows, int64_t out_features, int64_t in_features);
 int ddsp_hip_linear_weight_grad(const float* grad_y, int64_t dy_ld, const float* x, int64_t x_ld, float* grad_w,
                                 int64_t dw_ld, int64_t rows, int64_t out_features, int64_t in_features, void* ws,
