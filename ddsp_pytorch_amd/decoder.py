@@ -9,8 +9,8 @@ persistent launch per layer (core.gru), the two projections one matrix-core laun
 parameters in place (core.projections), and the synthesis section of ``forward`` (decoder.py:106-125) one
 fused launch before the reverb.  Under autograd the MLP blocks' Linears run their forward, input gradient
 and weight gradient on the matrix-core kernels (grad.LinearFn), their LayerNorm + LeakyReLU forward and
-backward on this package's kernels (grad.LNLeakyFn), the projections are one grad.LinearFn over the
-concatenated parameters (its weight gradient on the matrix cores), and the GRU's BPTT is one persistent
+backward on this package's kernels (grad.LNLeakyFn), the projections one grad.ProjectionsFn (forward in one
+matrix-core launch, weight gradient on the matrix cores), and the GRU's BPTT is one persistent
 launch with its weight gradients on the matrix cores.
 """
 import torch
@@ -198,17 +198,22 @@ def decoder_projections(self, hidden):
     hipBLASLt — nothing is cached on or rebound in the modules, so every write to a parameter, through
     ``.data`` included, is seen by the next call); the two outputs are column slices of one buffer, which
     the fused synthesis kernel reads with its row stride.  Under autograd the concatenated weights keep the call
-    differentiable, so the parameters receive their gradients as the reference's do (grad.LinearFn: the weight
-    gradient on ddsp_hip_linear_weight_grad, the GEMMs of 166 outputs on torch)."""
+    differentiable, so the parameters receive their gradients as the reference's do: at 512 inputs
+    grad.ProjectionsFn (the forward on ddsp_hip_projections, the weight gradient on ddsp_hip_linear_weight_grad),
+    elsewhere grad.LinearFn over the concatenated parameters."""
     hp, npj = self.harmonic_proj, self.noise_proj
     if not hidden.is_cuda or hp.bias is None or npj.bias is None or _hooked(hp) or _hooked(npj):
         return hp(hidden), npj(hidden)  # (module hooks see the calls the reference makes)
     ps = (hp.weight, hp.bias, npj.weight, npj.bias)
     h1, n = hp.out_features, hp.out_features + npj.out_features
     if torch.is_grad_enabled() and (hidden.requires_grad or any(p.requires_grad for p in ps)):
-        from .grad import LinearFn
-        w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
-        out = LinearFn.apply(hidden, w, b)
+        from .grad import LinearFn, ProjectionsFn
+        if hidden.shape[-1] == 512 and all(p.dtype == torch.float32 and p.dim() and p.stride(-1) == 1 for p in ps) \
+                and hidden.dtype == torch.float32 and hp.in_features == npj.in_features == 512:
+            out = ProjectionsFn.apply(hidden, hp.weight, hp.bias, npj.weight, npj.bias)
+        else:
+            w, b = torch.cat([hp.weight, npj.weight]), torch.cat([hp.bias, npj.bias])  # differentiable
+            out = LinearFn.apply(hidden, w, b)
         return out[..., :h1], out[..., h1:n]
     if _fp32_inference_ok(hidden, (hp, npj)):
         r = core.projections(hidden, hp, npj)

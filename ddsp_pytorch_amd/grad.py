@@ -463,6 +463,48 @@ class LinearFn(_F):
         return gx, gw, gb
 
 
+class ProjectionsFn(_F):
+    """decoder.py:106-117's harmonic_proj and noise_proj under autograd: the forward in ONE launch of
+    ddsp_hip_projections (both layers on the bf16 matrix cores, parameters read where they lie), returned as the
+    [..., n4] buffer the two outputs are column slices of; the backward dx = dy [W1; W2] on torch (166-wide K),
+    [dW1; dW2] on ddsp_hip_linear_weight_grad, the biases' sums on torch.  x [..., 512] (decoder_projections
+    checks; elsewhere it keeps one differentiable GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        K = x.shape[-1]
+        x2 = core._c(x).reshape(-1, K)
+        n1, n2 = w1.shape[0], w2.shape[0]
+        n4 = -(-(n1 + n2) // 4) * 4
+        y = torch.empty(x2.shape[0], n4, dtype=torch.float32, device=x.device)
+        w1c, w2c = core._c(w1), core._c(w2)
+        st = _lib.call("projections", _lib.ptr(x2), K, K, _lib.ptr(w1c), K, _lib.ptr(core._c(b1)), n1, _lib.ptr(w2c),
+                       K, _lib.ptr(core._c(b2)), n2, _lib.ptr(y), n4, x2.shape[0], _lib.stream_of(y),
+                       allow=(core.ERANGE,))
+        if st == core.ERANGE:  # (unaligned rows) one library GEMM
+            y[:, :n1 + n2] = torch.addmm(torch.cat([b1, b2]), x2, torch.cat([w1c, w2c]).t())
+        ctx.save_for_backward(x2, w1c, w2c)
+        ctx.x_shape = x.shape
+        return y.view(*x.shape[:-1], n4)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w1, w2 = ctx.saved_tensors
+        n1, n2 = w1.shape[0], w2.shape[0]
+        g = gy.reshape(-1, gy.shape[-1])[:, :n1 + n2].contiguous()
+        gx = gw1 = gb1 = gw2 = gb2 = None
+        if ctx.needs_input_grad[0]:
+            gx = g.mm(torch.cat([w1, w2])).view(ctx.x_shape)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            gw = core.linear_weight_grad(g, x2)
+            gw1, gw2 = gw[:n1], gw[n1:]
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[4]:
+            gb = g.sum(0)
+            gb1, gb2 = gb[:n1], gb[n1:]
+        return (gx, gw1 if ctx.needs_input_grad[1] else None, gb1 if ctx.needs_input_grad[2] else None,
+                gw2 if ctx.needs_input_grad[3] else None, gb2 if ctx.needs_input_grad[4] else None)
+
+
 class LNLeakyFn(_F):
     """LeakyReLU(LayerNorm(g)) under autograd for the decoder's MLP blocks (ddsp/core.py:122-129): the forward on
     ddsp_hip_layer_norm_leaky_relu, the backward — dg, dgamma, dbeta from the saved g — on

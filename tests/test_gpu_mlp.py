@@ -326,6 +326,36 @@ def test_linear_weight_grad_strides(dd):
     assert bool((dwb[:, :N] == 0).all()) and bool((dwb[:, N:] == 7.0).all())
 
 
+@pytest.mark.parametrize("rows", [12800, 37])
+def test_projections_fn_autograd(dd, rows):
+    """grad.ProjectionsFn (decoder.py:106-117's two projections under autograd: the forward on
+    ddsp_hip_projections, dx on torch, [dW1; dW2] on ddsp_hip_linear_weight_grad) against an fp64 evaluation:
+    both outputs and all five gradients within 2x of torch's fp32 Linears' error (RMS)."""
+    from ddsp_pytorch_amd.grad import ProjectionsFn
+    torch.manual_seed(rows)
+    l1, l2 = torch.nn.Linear(512, 101).cuda(), torch.nn.Linear(512, 65).cuda()
+    x = torch.randn(rows, 512, device="cuda")
+    g1, g2 = torch.randn(rows, 101, device="cuda"), torch.randn(rows, 65, device="cuda")
+    res = {}
+    for name in ("ours", "f32"):
+        xi = x.clone().requires_grad_(True)
+        ps = [t.detach().clone().requires_grad_(True) for t in (l1.weight, l1.bias, l2.weight, l2.bias)]
+        if name == "ours":
+            y = ProjectionsFn.apply(xi, *ps)
+            p, m = y[..., :101], y[..., 101:166]
+        else:
+            p, m = torch.nn.functional.linear(xi, ps[0], ps[1]), torch.nn.functional.linear(xi, ps[2], ps[3])
+        (p * g1).sum().add((m * g2).sum()).backward()
+        res[name] = [p.detach(), m.detach(), xi.grad] + [t.grad for t in ps]
+    xd = x.double()
+    W1, B1, W2, B2 = (t.detach().double() for t in (l1.weight, l1.bias, l2.weight, l2.bias))
+    G1, G2 = g1.double(), g2.double()
+    ref = [xd @ W1.t() + B1, xd @ W2.t() + B2, G1 @ W1 + G2 @ W2, G1.t() @ xd, G1.sum(0), G2.t() @ xd, G2.sum(0)]
+    rms = lambda e: float(e.pow(2).mean().sqrt())
+    for i, (ours, f32, r) in enumerate(zip(res["ours"], res["f32"], ref)):
+        assert rms(ours.double() - r) <= 2 * rms(f32.double() - r) + 1e-12, (i, rms(ours.double() - r), rms(f32.double() - r))
+
+
 def test_mlp_autograd_route(dd, monkeypatch):
     """Under autograd the decoder's MLPs (mlp_forward) run each block's Linear on LinearFn — the 512-input blocks'
     forward and input gradient on the matrix-core kernel — and match torch's modules (values and every
